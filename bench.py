@@ -1,0 +1,261 @@
+#!/usr/bin/env python3
+"""bench.py -- device-resident chunk-hash throughput (BASELINE.json metric).
+
+Workload per GPU (configs[1], "C2"): one 4 GiB synthetic file at 256 KiB chunks
+(16,384 chunks), bytes generated directly in HBM before timing.  One step = one
+launch of the chunk-hash kernel over the whole batch (SHA-1 of every chunk,
+20-byte digests written to HBM).  With N GPUs each rank hashes its own 4 GiB
+shard of an N x 4 GiB file (weak scaling, contiguous chunk ranges, no data-path
+collective; the only collectives are the timing barrier and the max-over-ranks
+reduction).
+
+Launch:  python bench.py [--gpus N --steps K --warmup W]
+   N>1:  python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+Rank 0 prints ONE JSON line.
+"""
+import argparse
+import hashlib
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402  (first: one HIP runtime per process)
+
+from bitflood_amd import DeviceBuffer, b64_27  # noqa: E402
+from bitflood_amd import hashing as H  # noqa: E402
+
+GIB = 1 << 30
+SEED_C = 0x5EED
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak, MI355X_MICROARCH.md "Chip-level parameters"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--chunk-size", type=int, default=262144)
+    ap.add_argument("--file-gib", type=float, default=4.0, help="bytes hashed per GPU per step")
+    ap.add_argument("--variant", type=int, default=0, help="kernel variant (0 = automatic)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, os.cpu_count())")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the host->device->host rate")
+    return ap.parse_args()
+
+
+def dist_setup(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    if args.gpus != world:
+        if rank == 0:
+            print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using {world}", file=sys.stderr)
+    return rank, world, local
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def max_over_ranks(x, world):
+    if world == 1:
+        return x
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def traffic_from_profiles(file_bytes):
+    """HBM bytes per launch measured with rocprofv3 PMC (FETCH_SIZE x2, gfx950
+    correction), recorded by tools/pmc_traffic.py."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        if int(d.get("file_bytes", -1)) == int(file_bytes):
+            return float(d["hbm_bytes_per_launch"])
+    except Exception:
+        pass
+    return None
+
+
+def cpu_baseline(args, stream_start, n_chunks_sample, gpu_digests_sample):
+    """The oracle restatement of the reference encoder hash (portable C -O2,
+    oracle/sha1_oracle.c) on the host cores, over a bounded sample of the same
+    synthetic bytes.  kind="port": building the reference was denied
+    (SURVEY.md §8c)."""
+    from tests.oracle_lib import Oracle
+    orc = Oracle()
+    cs = args.chunk_size
+    nbytes = n_chunks_sample * cs
+    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    data = orc.synth(SEED_C, stream_start, nbytes, nthreads=threads)
+    offs = np.arange(n_chunks_sample, dtype=np.uint64) * np.uint64(cs)
+    sizes = np.full(n_chunks_sample, cs, dtype=np.uint32)
+    # all host cores, chunk-parallel
+    reps, t_mt = 0, 0.0
+    while t_mt < 3.0 and reps < 20:
+        t0 = time.perf_counter()
+        d_mt = orc.sha1_batch(data, offs, sizes, nthreads=threads)
+        t_mt += time.perf_counter() - t0
+        reps += 1
+    mt_gibs = reps * nbytes / GIB / t_mt
+    # one thread, like Encoder.cpp:40-79 (bounded to 1/4 of the sample)
+    n1 = max(1, n_chunks_sample // 4)
+    t0 = time.perf_counter()
+    d_1 = orc.sha1_batch(data, offs[:n1], sizes[:n1], nthreads=1)
+    t_1 = time.perf_counter() - t0
+    st_gibs = n1 * cs / GIB / t_1
+    parity = bool(np.array_equal(d_mt, gpu_digests_sample) and np.array_equal(d_1, gpu_digests_sample[:n1]))
+    return {
+        "value": round(mt_gibs, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+        "sample": f"{n_chunks_sample} x {cs // 1024} KiB chunks ({nbytes / GIB:.2f} GiB) of the same stream, "
+                  f"{reps} pass(es) on {threads} threads; single-thread pass over {n1} chunks",
+        "single_thread_value": round(st_gibs, 3),
+        "host": _host_desc(),
+        "parity_vs_gpu": parity,
+    }, data
+
+
+def _host_desc():
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except Exception:
+        pass
+    return {"cpu_model": model, "os_cpu_count": os.cpu_count()}
+
+
+def e2e_rate(host_data, cs):
+    """Host bytes in -> host digests out through the lbf_ctx pinned pipeline
+    (PCIe-inclusive rate for DESIGN.md; never the headline value)."""
+    from bitflood_amd import ChunkHasher, chunk_table
+    offs, sizes = chunk_table(host_data.size, cs)
+    with ChunkHasher(device_mask=1) as h:
+        h.hash_chunks(host_data[: 64 * cs], offs[:64], sizes[:64])  # warm
+        t0 = time.perf_counter()
+        d = h.hash_chunks(host_data, offs, sizes)
+        t = time.perf_counter() - t0
+    return host_data.size / GIB / t, d
+
+
+def main():
+    args = parse()
+    rank, world, local = dist_setup(args)
+    if args.variant:
+        H.set_kernel_variant(args.variant)
+    cs = args.chunk_size
+    file_bytes = int(args.file_gib * GIB)
+    n_chunks = (file_bytes + cs - 1) // cs
+    stream_start = rank * file_bytes  # this rank's shard of the N x 4 GiB file
+
+    buf = DeviceBuffer(file_bytes)
+    dig = DeviceBuffer(n_chunks * 20)
+    stream = torch.cuda.current_stream()
+    sptr = stream.cuda_stream
+    buf.fill_synthetic(SEED_C, start=stream_start, stream=sptr)
+    torch.cuda.synchronize()
+
+    def step():
+        H.uniform_launch(buf, file_bytes, cs, 0, n_chunks, dig, stream=sptr)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    barrier(world)
+    torch.cuda.synchronize()
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(args.steps):
+        step()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    barrier(world)
+    t1 = time.perf_counter()
+    wall = t1 - t0
+    ev_ms = e0.elapsed_time(e1)
+    t_max = max_over_ranks(wall, world)
+    ev_max = max_over_ranks(ev_ms, world)
+
+    total_bytes = world * file_bytes * args.steps
+    value = total_bytes / GIB / t_max
+    launch_s = ev_max / 1e3 / args.steps
+    achieved_gbs = file_bytes / launch_s / 1e9
+
+    digests = dig.download(n_chunks * 20).reshape(n_chunks, 20)
+    out = None
+    if rank == 0:
+        out = {
+            "metric": "GiB/s device-resident chunk hashing, 256 KiB chunks, at 1/2/4/8 MI355X",
+            "value": round(value, 3),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(t_max * 1e3 / args.steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic: counter-mode splitmix64 stream seed 0x5EED generated in HBM "
+                    "(rank r hashes bytes [r*4GiB,(r+1)*4GiB) of it)",
+            "config": {
+                "workload": "C2 per GPU: one 4 GiB file, 256 KiB chunks, SHA-1 -> 20 B digest per chunk "
+                            "(BASELINE.json configs[1]); N GPUs = N x 4 GiB file, contiguous chunk shards",
+                "file_bytes_per_gpu": file_bytes,
+                "chunk_size": cs,
+                "chunks_per_gpu": n_chunks,
+                "kernel_variant": H.load().lbf_get_kernel_variant(),
+                "parallelism": f"chunk-shard x{world} (no data-path collective)",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved_gbs, 2),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
+                "traffic": traffic_from_profiles(file_bytes),
+                "kernel_ms": round(launch_s * 1e3, 4),
+                "algorithmic_bytes_per_launch": file_bytes,
+            },
+            "digest_check": hashlib.sha1(digests.tobytes()).hexdigest(),
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            sample = min(n_chunks, 4096)
+            cb, host = cpu_baseline(args, stream_start, sample, digests[:sample])
+            out["cpu_baseline"] = cb
+            if not args.no_e2e:
+                rate, d_e2e = e2e_rate(host, cs)
+                out["e2e_host_to_host_gibs"] = round(rate, 3)
+                out["e2e_parity"] = bool(np.array_equal(d_e2e, digests[:sample]))
+        out["first_chunk_b64"] = b64_27(bytes(digests[0]))
+    buf.free()
+    dig.free()
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

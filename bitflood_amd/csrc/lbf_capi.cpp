@@ -1,0 +1,482 @@
+// lbf_capi.cpp -- host side of liblbfhash.so: error slot, base64-27, device
+// helpers and the lbf_ctx that streams host chunks through pinned staging to
+// one or more MI355X devices.
+//
+// The context is the batched replacement for the reference's per-chunk
+// fread -> Base64Encode loop (/root/reference/cpp/src/Encoder.cpp:54-72) and
+// the per-chunk verify loops (Flood.cpp:246-285, ChunkMethods.cpp:111-128,
+// 156-167): the caller hands over a descriptor table, the context copies the
+// covered byte ranges into device slots (double-buffered: host memcpy of group
+// g+1 overlaps H2D + kernel + D2H of group g) and returns digests or verdicts.
+// Multiple devices take contiguous index ranges, one host thread each, with no
+// collective.
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "lbf_internal.hpp"
+
+namespace lbf {
+
+namespace {
+thread_local std::string t_last_error;
+}
+
+void set_error(const std::string& msg) { t_last_error = msg; }
+const char* last_error_cstr() { return t_last_error.c_str(); }
+
+int fail(int status, const std::string& msg) {
+  set_error(msg);
+  return status;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+  return fail(e == hipErrorOutOfMemory ? LBF_ERR_NOMEM : LBF_ERR_HIP,
+              std::string(what) + ": " + hipGetErrorString(e));
+}
+
+}  // namespace lbf
+
+using lbf::fail;
+
+// ---------------------------------------------------------------------------
+// base64-27 (BaseN_Encoder(alphabet, 6), no padding: basecode.cpp:13-37,39-104;
+// alphabet Encoder.cpp:104-105).  20 bytes = 160 bits = 26 full sextets plus
+// one 4-bit tail sextet, MSB first, zero-filled on the right.
+// ---------------------------------------------------------------------------
+static const char kAlphabet[] = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/";
+
+extern "C" void lbf_b64_27(const uint8_t digest[20], char out[28]) {
+  int o = 0;
+  // 6 groups of 3 bytes -> 24 chars, then 2 bytes -> 3 chars (last one partial)
+  for (int g = 0; g < 6; ++g) {
+    const uint32_t v = (uint32_t(digest[3 * g]) << 16) | (uint32_t(digest[3 * g + 1]) << 8) | digest[3 * g + 2];
+    out[o++] = kAlphabet[(v >> 18) & 63];
+    out[o++] = kAlphabet[(v >> 12) & 63];
+    out[o++] = kAlphabet[(v >> 6) & 63];
+    out[o++] = kAlphabet[v & 63];
+  }
+  const uint32_t v = (uint32_t(digest[18]) << 8) | digest[19];  // 16 bits
+  out[o++] = kAlphabet[(v >> 10) & 63];
+  out[o++] = kAlphabet[(v >> 4) & 63];
+  out[o++] = kAlphabet[(v << 2) & 63];
+  out[o] = '\0';
+}
+
+static int b64_value(char c) {
+  if (c >= 'A' && c <= 'Z') return c - 'A';
+  if (c >= 'a' && c <= 'z') return c - 'a' + 26;
+  if (c >= '0' && c <= '9') return c - '0' + 52;
+  if (c == '+') return 62;
+  if (c == '/') return 63;
+  return -1;
+}
+
+extern "C" int lbf_b64_27_decode(const char* in, size_t len, uint8_t out[20]) {
+  if (!in || !out || len != 27) return fail(LBF_ERR_INVALID, "b64_27_decode: need exactly 27 chars");
+  uint32_t acc = 0;
+  int bits = 0, o = 0;
+  for (size_t i = 0; i < 27; ++i) {
+    const int v = b64_value(in[i]);
+    if (v < 0) return fail(LBF_ERR_INVALID, "b64_27_decode: character outside the alphabet");
+    acc = (acc << 6) | (uint32_t)v;
+    bits += 6;
+    if (bits >= 8) {
+      bits -= 8;
+      if (o < 20) out[o++] = (uint8_t)(acc >> bits);
+      acc &= (1u << bits) - 1u;
+    }
+  }
+  // 162 bits read, 160 used: the 2 leftover bits must be zero (canonical form)
+  if (o != 20 || bits != 2 || acc != 0) return fail(LBF_ERR_INVALID, "b64_27_decode: non-canonical tail");
+  return LBF_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Library / device helpers
+// ---------------------------------------------------------------------------
+extern "C" int lbf_abi_version(void) { return LBF_ABI_VERSION; }
+
+extern "C" const char* lbf_last_error(void) { return lbf::last_error_cstr(); }
+
+extern "C" int lbf_device_count(int* out) {
+  if (!out) return fail(LBF_ERR_INVALID, "null out");
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+  *out = n;
+  return LBF_OK;
+}
+
+extern "C" int lbf_dev_malloc(void** out, uint64_t bytes) {
+  if (!out) return fail(LBF_ERR_INVALID, "null out");
+  LBF_HIP_TRY(hipMalloc(out, bytes ? bytes : 1));
+  return LBF_OK;
+}
+extern "C" int lbf_dev_free(void* p) {
+  LBF_HIP_TRY(hipFree(p));
+  return LBF_OK;
+}
+extern "C" int lbf_memcpy_h2d(void* dst, const void* src, uint64_t bytes) {
+  LBF_HIP_TRY(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+  return LBF_OK;
+}
+extern "C" int lbf_memcpy_d2h(void* dst, const void* src, uint64_t bytes) {
+  LBF_HIP_TRY(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+  return LBF_OK;
+}
+extern "C" int lbf_set_device(int d) {
+  LBF_HIP_TRY(hipSetDevice(d));
+  return LBF_OK;
+}
+extern "C" int lbf_device_synchronize(void) {
+  LBF_HIP_TRY(hipDeviceSynchronize());
+  return LBF_OK;
+}
+extern "C" int lbf_stream_create(void** out) {
+  if (!out) return fail(LBF_ERR_INVALID, "null out");
+  hipStream_t s;
+  LBF_HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  *out = (void*)s;
+  return LBF_OK;
+}
+extern "C" int lbf_stream_destroy(void* s) {
+  LBF_HIP_TRY(hipStreamDestroy((hipStream_t)s));
+  return LBF_OK;
+}
+extern "C" int lbf_stream_synchronize(void* s) {
+  LBF_HIP_TRY(hipStreamSynchronize((hipStream_t)s));
+  return LBF_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Context: per-device workers with two pipeline slots each.
+// ---------------------------------------------------------------------------
+namespace {
+
+struct Slot {
+  hipStream_t stream = nullptr;
+  uint8_t* d_data = nullptr;       // slot_bytes
+  uint64_t* d_off = nullptr;       // desc_cap
+  uint32_t* d_size = nullptr;
+  uint8_t* d_dig = nullptr;        // desc_cap * 20
+  uint8_t* d_exp = nullptr;
+  uint8_t* d_ver = nullptr;        // desc_cap
+  uint8_t* h_data = nullptr;       // pinned, slot_bytes
+  uint64_t* h_off = nullptr;       // pinned
+  uint32_t* h_size = nullptr;
+  uint8_t* h_dig = nullptr;
+  uint8_t* h_exp = nullptr;
+  uint8_t* h_ver = nullptr;
+  // pending group to finalize after the stream drains
+  bool pending = false;
+  uint64_t g_begin = 0, g_end = 0;
+};
+
+struct Worker {
+  int device = 0;
+  Slot slot[2];
+  uint64_t slot_bytes = 0;
+  uint64_t desc_cap = 0;
+};
+
+}  // namespace
+
+struct lbf_ctx {
+  std::vector<Worker> workers;
+  std::mutex mu;
+};
+
+namespace {
+
+uint64_t env_u64(const char* name, uint64_t dflt) {
+  const char* v = getenv(name);
+  if (!v || !*v) return dflt;
+  return strtoull(v, nullptr, 10);
+}
+
+int worker_init(Worker& w, int device) {
+  w.device = device;
+  w.slot_bytes = env_u64("LBF_SLOT_MB", 256) << 20;
+  w.desc_cap = 1u << 16;
+  LBF_HIP_TRY(hipSetDevice(device));
+  for (Slot& s : w.slot) {
+    LBF_HIP_TRY(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+    LBF_HIP_TRY(hipMalloc((void**)&s.d_data, w.slot_bytes));
+    LBF_HIP_TRY(hipMalloc((void**)&s.d_off, w.desc_cap * 8));
+    LBF_HIP_TRY(hipMalloc((void**)&s.d_size, w.desc_cap * 4));
+    LBF_HIP_TRY(hipMalloc((void**)&s.d_dig, w.desc_cap * 20));
+    LBF_HIP_TRY(hipMalloc((void**)&s.d_exp, w.desc_cap * 20));
+    LBF_HIP_TRY(hipMalloc((void**)&s.d_ver, w.desc_cap));
+    LBF_HIP_TRY(hipHostMalloc((void**)&s.h_data, w.slot_bytes, hipHostMallocDefault));
+    LBF_HIP_TRY(hipHostMalloc((void**)&s.h_off, w.desc_cap * 8, hipHostMallocDefault));
+    LBF_HIP_TRY(hipHostMalloc((void**)&s.h_size, w.desc_cap * 4, hipHostMallocDefault));
+    LBF_HIP_TRY(hipHostMalloc((void**)&s.h_dig, w.desc_cap * 20, hipHostMallocDefault));
+    LBF_HIP_TRY(hipHostMalloc((void**)&s.h_exp, w.desc_cap * 20, hipHostMallocDefault));
+    LBF_HIP_TRY(hipHostMalloc((void**)&s.h_ver, w.desc_cap, hipHostMallocDefault));
+  }
+  return LBF_OK;
+}
+
+void worker_free(Worker& w) {
+  if (hipSetDevice(w.device) != hipSuccess) return;
+  for (Slot& s : w.slot) {
+    if (s.stream) hipStreamSynchronize(s.stream);
+    hipFree(s.d_data); hipFree(s.d_off); hipFree(s.d_size);
+    hipFree(s.d_dig); hipFree(s.d_exp); hipFree(s.d_ver);
+    hipHostFree(s.h_data); hipHostFree(s.h_off); hipHostFree(s.h_size);
+    hipHostFree(s.h_dig); hipHostFree(s.h_exp); hipHostFree(s.h_ver);
+    if (s.stream) hipStreamDestroy(s.stream);
+    s = Slot{};
+  }
+}
+
+struct Job {
+  const uint8_t* base;
+  uint64_t base_len;
+  const uint64_t* offsets;
+  const uint32_t* sizes;
+  const uint8_t* expected;  // null => hash mode
+  uint8_t* digests;         // hash mode output
+  uint8_t* verdicts;        // verify mode output
+};
+
+// Copy finished results of a slot's group to the caller's arrays.
+void finalize(const Job& job, Slot& s) {
+  if (!s.pending) return;
+  const uint64_t cnt = s.g_end - s.g_begin;
+  if (job.expected) memcpy(job.verdicts + s.g_begin, s.h_ver, cnt);
+  else memcpy(job.digests + 20 * s.g_begin, s.h_dig, cnt * 20);
+  s.pending = false;
+}
+
+// Hash one chunk that does not fit a slot: dedicated device buffer.
+int run_oversize(Worker& w, const Job& job, uint64_t i) {
+  Slot& s = w.slot[0];
+  LBF_HIP_TRY(hipStreamSynchronize(s.stream));
+  const uint32_t sz = job.sizes[i];
+  uint8_t* d = nullptr;
+  LBF_HIP_TRY(hipMalloc((void**)&d, sz ? sz : 1));
+  int rc = LBF_OK;
+  do {
+    if (hipMemcpy(d, job.base + job.offsets[i], sz, hipMemcpyHostToDevice) != hipSuccess) {
+      rc = fail(LBF_ERR_HIP, "oversize chunk H2D failed");
+      break;
+    }
+    s.h_off[0] = 0;
+    s.h_size[0] = sz;
+    if (hipMemcpy(s.d_off, s.h_off, 8, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(s.d_size, s.h_size, 4, hipMemcpyHostToDevice) != hipSuccess) {
+      rc = fail(LBF_ERR_HIP, "oversize descriptor H2D failed");
+      break;
+    }
+    if (job.expected) {
+      memcpy(s.h_exp, job.expected + 20 * i, 20);
+      if (hipMemcpy(s.d_exp, s.h_exp, 20, hipMemcpyHostToDevice) != hipSuccess) {
+        rc = fail(LBF_ERR_HIP, "oversize expected H2D failed");
+        break;
+      }
+    }
+    rc = lbf_sha1_launch(d, s.d_off, s.d_size, 1, job.expected ? nullptr : s.d_dig,
+                         job.expected ? s.d_exp : nullptr, job.expected ? s.d_ver : nullptr, s.stream);
+    if (rc) break;
+    if (hipStreamSynchronize(s.stream) != hipSuccess) {
+      rc = fail(LBF_ERR_HIP, "oversize kernel failed");
+      break;
+    }
+    if (job.expected) {
+      if (hipMemcpy(job.verdicts + i, s.d_ver, 1, hipMemcpyDeviceToHost) != hipSuccess) rc = LBF_ERR_HIP;
+    } else {
+      if (hipMemcpy(job.digests + 20 * i, s.d_dig, 20, hipMemcpyDeviceToHost) != hipSuccess) rc = LBF_ERR_HIP;
+    }
+  } while (0);
+  hipFree(d);
+  return rc;
+}
+
+// Process descriptors [begin, end) on one device.
+int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
+  LBF_HIP_TRY(hipSetDevice(w.device));
+  int cur = 0;
+  uint64_t i = begin;
+  int rc = LBF_OK;
+  while (i < end && rc == LBF_OK) {
+    // Oversize chunk: its own path (slots drained first).
+    if ((uint64_t)job.sizes[i] + 15 > w.slot_bytes) {
+      for (Slot& s : w.slot) {
+        LBF_HIP_TRY(hipStreamSynchronize(s.stream));
+        finalize(job, s);
+      }
+      rc = run_oversize(w, job, i);
+      ++i;
+      continue;
+    }
+    // Group: consecutive descriptors whose covering range fits one slot.
+    uint64_t lo = job.offsets[i], hi = lo + job.sizes[i];
+    uint64_t j = i + 1;
+    while (j < end && j - i < w.desc_cap) {
+      const uint64_t o = job.offsets[j], e = o + job.sizes[j];
+      const uint64_t nlo = std::min(lo, o), nhi = std::max(hi, e);
+      if (nhi - nlo + 15 > w.slot_bytes) break;
+      lo = nlo;
+      hi = nhi;
+      ++j;
+    }
+    Slot& s = w.slot[cur];
+    LBF_HIP_TRY(hipStreamSynchronize(s.stream));
+    finalize(job, s);
+    const uint64_t cnt = j - i;
+    // Stage bytes and rebased descriptors in pinned memory.  The covered range
+    // [lo, hi) lands at h_data + (lo % 16) so each chunk keeps its offset's
+    // 16-byte phase (aligned chunks take the vector-load path on the device).
+    const uint64_t shift = lo & 15u;
+    memcpy(s.h_data + shift, job.base + lo, hi - lo);
+    for (uint64_t k = 0; k < cnt; ++k) {
+      s.h_off[k] = job.offsets[i + k] - lo + shift;
+      s.h_size[k] = job.sizes[i + k];
+    }
+    const uint64_t copy_bytes = hi - lo + shift;
+    LBF_HIP_TRY(hipMemcpyAsync(s.d_data, s.h_data, copy_bytes, hipMemcpyHostToDevice, s.stream));
+    LBF_HIP_TRY(hipMemcpyAsync(s.d_off, s.h_off, cnt * 8, hipMemcpyHostToDevice, s.stream));
+    LBF_HIP_TRY(hipMemcpyAsync(s.d_size, s.h_size, cnt * 4, hipMemcpyHostToDevice, s.stream));
+    if (job.expected) {
+      memcpy(s.h_exp, job.expected + 20 * i, cnt * 20);
+      LBF_HIP_TRY(hipMemcpyAsync(s.d_exp, s.h_exp, cnt * 20, hipMemcpyHostToDevice, s.stream));
+      rc = lbf_sha1_launch(s.d_data, s.d_off, s.d_size, cnt, nullptr, s.d_exp, s.d_ver, s.stream);
+      if (rc) break;
+      LBF_HIP_TRY(hipMemcpyAsync(s.h_ver, s.d_ver, cnt, hipMemcpyDeviceToHost, s.stream));
+    } else {
+      rc = lbf_sha1_launch(s.d_data, s.d_off, s.d_size, cnt, s.d_dig, nullptr, nullptr, s.stream);
+      if (rc) break;
+      LBF_HIP_TRY(hipMemcpyAsync(s.h_dig, s.d_dig, cnt * 20, hipMemcpyDeviceToHost, s.stream));
+    }
+    s.pending = true;
+    s.g_begin = i;
+    s.g_end = j;
+    cur ^= 1;
+    i = j;
+  }
+  for (Slot& s : w.slot) {
+    if (hipStreamSynchronize(s.stream) != hipSuccess && rc == LBF_OK)
+      rc = fail(LBF_ERR_HIP, "stream synchronize failed");
+    if (rc == LBF_OK) finalize(job, s);
+    s.pending = false;
+  }
+  return rc;
+}
+
+int validate_host_job(const Job& job, uint64_t n) {
+  for (uint64_t i = 0; i < n; ++i) {
+    const uint64_t o = job.offsets[i], sz = job.sizes[i];
+    if (o > job.base_len || sz > job.base_len - o)
+      return fail(LBF_ERR_INVALID, "chunk " + std::to_string(i) + " lies outside [base, base+base_len)");
+  }
+  return LBF_OK;
+}
+
+int run_job(lbf_ctx* ctx, const Job& job, uint64_t n) {
+  if (int rc = validate_host_job(job, n)) return rc;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  const size_t nw = ctx->workers.size();
+  if (nw == 1 || n < 2 * nw) return worker_run(ctx->workers[0], job, 0, n);
+  std::vector<int> rcs(nw, LBF_OK);
+  std::vector<std::string> errs(nw);
+  std::vector<std::thread> th;
+  for (size_t d = 0; d < nw; ++d) {
+    const uint64_t b = n * d / nw, e = n * (d + 1) / nw;
+    th.emplace_back([&, d, b, e] {
+      rcs[d] = worker_run(ctx->workers[d], job, b, e);
+      if (rcs[d]) errs[d] = lbf_last_error();
+    });
+  }
+  for (auto& t : th) t.join();
+  for (size_t d = 0; d < nw; ++d)
+    if (rcs[d]) return fail(rcs[d], "device " + std::to_string(ctx->workers[d].device) + ": " + errs[d]);
+  return LBF_OK;
+}
+
+// Device-pointer batch: synchronous on worker 0's first stream.
+int run_device_job(lbf_ctx* ctx, const uint8_t* base, const uint64_t* offsets, const uint32_t* sizes,
+                   uint64_t n, uint8_t* digests, const uint8_t* expected, uint8_t* verdicts) {
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  Worker& w = ctx->workers[0];
+  LBF_HIP_TRY(hipSetDevice(w.device));
+  hipStream_t s = w.slot[0].stream;
+  for (uint64_t i = 0; i < n; i += 0xFFFFFFFFull) {
+    const uint64_t cnt = std::min<uint64_t>(n - i, 0xFFFFFFFFull);
+    int rc = lbf_sha1_launch(base, offsets + i, sizes + i, cnt, digests ? digests + 20 * i : nullptr,
+                             expected ? expected + 20 * i : nullptr, verdicts ? verdicts + i : nullptr, s);
+    if (rc) return rc;
+  }
+  LBF_HIP_TRY(hipStreamSynchronize(s));
+  return LBF_OK;
+}
+
+}  // namespace
+
+extern "C" int lbf_ctx_create(uint32_t device_mask, lbf_ctx** out) {
+  if (!out) return fail(LBF_ERR_INVALID, "null out");
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+    return fail(LBF_ERR_NO_DEVICE, "no GPU visible: the chunk-hash path runs only on MI355X (no CPU fallback)");
+  lbf_ctx* ctx = new lbf_ctx();
+  for (int d = 0; d < ndev && d < 32; ++d) {
+    if (device_mask && !(device_mask & (1u << d))) continue;
+    ctx->workers.emplace_back();
+    if (int rc = worker_init(ctx->workers.back(), d)) {
+      std::string msg = lbf_last_error();
+      lbf_ctx_destroy(ctx);
+      return fail(rc, msg);
+    }
+  }
+  if (ctx->workers.empty()) {
+    delete ctx;
+    return fail(LBF_ERR_NO_DEVICE, "device_mask selects no visible device");
+  }
+  *out = ctx;
+  return LBF_OK;
+}
+
+extern "C" void lbf_ctx_destroy(lbf_ctx* ctx) {
+  if (!ctx) return;
+  for (Worker& w : ctx->workers) worker_free(w);
+  delete ctx;
+}
+
+extern "C" int lbf_ctx_num_devices(const lbf_ctx* ctx) { return ctx ? (int)ctx->workers.size() : 0; }
+
+extern "C" int lbf_sha1_batch(lbf_ctx* ctx, const uint8_t* base, uint64_t base_len, const uint64_t* offsets,
+                              const uint32_t* sizes, uint64_t n, uint8_t* out_digests, int flags) {
+  if (!ctx) return fail(LBF_ERR_INVALID, "null context");
+  if (n == 0) return LBF_OK;
+  if (!base || !offsets || !sizes || !out_digests) return fail(LBF_ERR_INVALID, "null argument");
+  if (flags == LBF_DEVICE_PTR) return run_device_job(ctx, base, offsets, sizes, n, out_digests, nullptr, nullptr);
+  if (flags != LBF_HOST_PTR) return fail(LBF_ERR_INVALID, "unknown flags");
+  Job job{base, base_len, offsets, sizes, nullptr, out_digests, nullptr};
+  return run_job(ctx, job, n);
+}
+
+extern "C" int lbf_verify_batch(lbf_ctx* ctx, const uint8_t* base, uint64_t base_len, const uint64_t* offsets,
+                                const uint32_t* sizes, uint64_t n, const uint8_t* expected, uint8_t* verdicts,
+                                int flags) {
+  if (!ctx) return fail(LBF_ERR_INVALID, "null context");
+  if (n == 0) return LBF_OK;
+  if (!base || !offsets || !sizes || !expected || !verdicts) return fail(LBF_ERR_INVALID, "null argument");
+  if (flags == LBF_DEVICE_PTR) return run_device_job(ctx, base, offsets, sizes, n, nullptr, expected, verdicts);
+  if (flags != LBF_HOST_PTR) return fail(LBF_ERR_INVALID, "unknown flags");
+  Job job{base, base_len, offsets, sizes, expected, nullptr, verdicts};
+  return run_job(ctx, job, n);
+}
+
+extern "C" int lbf_sha1_one(lbf_ctx* ctx, const uint8_t* data, uint32_t size, uint8_t out[20]) {
+  static const uint8_t kEmpty = 0;
+  if (!data && size) return fail(LBF_ERR_INVALID, "null data");
+  const uint64_t off = 0;
+  return lbf_sha1_batch(ctx, data ? data : &kEmpty, size, &off, &size, 1, out, LBF_HOST_PTR);
+}

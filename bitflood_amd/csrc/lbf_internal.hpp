@@ -1,0 +1,40 @@
+// lbf_internal.hpp -- shared internals of liblbfhash.so (not part of the ABI).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+
+#include "lbf_hash.h"
+
+namespace lbf {
+
+// Thread-local last-error slot behind lbf_last_error().
+void set_error(const std::string& msg);
+int fail(int status, const std::string& msg);
+int hip_fail(hipError_t e, const char* what);
+
+#define LBF_HIP_TRY(expr)                                   \
+  do {                                                      \
+    hipError_t lbf_e_ = (expr);                             \
+    if (lbf_e_ != hipSuccess) return ::lbf::hip_fail(lbf_e_, #expr); \
+  } while (0)
+
+// Kernel-side parameter block shared by every chunk-hash kernel variant.
+struct ChunkParams {
+  const uint8_t* base;
+  const uint64_t* offsets;   // null => uniform chunking of [0, len)
+  const uint32_t* sizes;
+  uint64_t len;              // uniform: region length
+  uint64_t first_chunk;      // uniform: index of chunk 0 of this launch
+  uint32_t chunk_size;       // uniform
+  uint32_t n;                // chunks in this launch
+  uint8_t* digests;          // n*20 bytes or null
+  const uint8_t* expected;   // n*20 bytes or null
+  uint8_t* verdicts;         // n bytes or null
+};
+
+int launch_chunks(const ChunkParams& p, hipStream_t stream);
+
+}  // namespace lbf

@@ -1,0 +1,178 @@
+// sha1_device.hpp -- SHA-1 building blocks for the CDNA4 (gfx950) chunk-hash kernels.
+//
+// Semantics follow the reference's hash exactly (Crypto++ 5.2.1 SHA via
+// Encoder::Base64Encode, /root/reference/cpp/src/Encoder.cpp:107-120):
+//   init state           cpp/extern/crypto++/5.2.1/sha.cpp:19-26
+//   80-round compression  sha.cpp:28-79 (f1 choose, f2/f4 parity, f3 majority)
+//   big-endian words      iterhash.h:123-132 (ByteReverse on little-endian hosts)
+//   0x80 pad + 64-bit big-endian bit length in words 14-15, one or two final
+//   blocks                iterhash.cpp:86-99, iterhash.h:30-31,106-121
+//
+// Everything here is 32-bit integer VALU work: rotates lower to v_alignbit_b32,
+// the three round functions and the schedule's 3-way xor to gfx950's
+// v_bitop3_b32, byte swaps to v_perm_b32, the 5-term round sums to two
+// v_add3_u32.  No MFMA: hashing is not a contraction.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace lbf {
+
+constexpr uint32_t kH0 = 0x67452301u;
+constexpr uint32_t kH1 = 0xEFCDAB89u;
+constexpr uint32_t kH2 = 0x98BADCFEu;
+constexpr uint32_t kH3 = 0x10325476u;
+constexpr uint32_t kH4 = 0xC3D2E1F0u;
+
+constexpr uint32_t kK1 = 0x5A827999u;  // rounds  0-19 (R0/R1)
+constexpr uint32_t kK2 = 0x6ED9EBA1u;  // rounds 20-39 (R2)
+constexpr uint32_t kK3 = 0x8F1BBCDCu;  // rounds 40-59 (R3)
+constexpr uint32_t kK4 = 0xCA62C1D6u;  // rounds 60-79 (R4)
+
+__device__ __forceinline__ uint32_t rotl(uint32_t x, int n) { return (x << n) | (x >> (32 - n)); }
+
+__device__ __forceinline__ uint32_t bswap(uint32_t x) { return __builtin_bswap32(x); }
+
+// gfx950 v_bitop3_b32 evaluates any 3-input bitwise function in one VALU op:
+// result bit = LUT[(S0<<2)|(S1<<1)|S2], i.e. LUT = f(0xF0, 0xCC, 0xAA).
+constexpr uint32_t kLutChoose = 0xCA;  // (b & c) | (~b & d)          f1, sha.cpp:28
+constexpr uint32_t kLutParity = 0x96;  // b ^ c ^ d                    f2/f4, sha.cpp:29,31
+constexpr uint32_t kLutMajor = 0xE8;   // (b & c) | (d & (b | c))     f3, sha.cpp:30
+
+template <uint32_t kLut>
+__device__ __forceinline__ uint32_t bitop3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, kLut);
+}
+__device__ __forceinline__ uint32_t f_choose(uint32_t b, uint32_t c, uint32_t d) {
+  return bitop3<kLutChoose>(b, c, d);
+}
+__device__ __forceinline__ uint32_t f_major(uint32_t b, uint32_t c, uint32_t d) {
+  return bitop3<kLutMajor>(b, c, d);
+}
+__device__ __forceinline__ uint32_t f_parity(uint32_t b, uint32_t c, uint32_t d) {
+  return bitop3<kLutParity>(b, c, d);
+}
+// blk1 (sha.cpp:15): rotl(w[i-3] ^ w[i-8] ^ w[i-14] ^ w[i-16], 1)
+__device__ __forceinline__ uint32_t sched(uint32_t w3, uint32_t w8, uint32_t w14, uint32_t w16) {
+  return rotl(bitop3<kLutParity>(w3, w8, w14) ^ w16, 1);
+}
+
+struct Digest {
+  uint32_t h[5];
+  __device__ __forceinline__ void init() {
+    h[0] = kH0; h[1] = kH1; h[2] = kH2; h[3] = kH3; h[4] = kH4;
+  }
+};
+
+// One compression of a 16-word big-endian block.  `w` is consumed as the
+// 16-word rolling message schedule (the blk1 window of sha.cpp:15).
+__device__ __forceinline__ void compress(Digest& s, uint32_t (&w)[16]) {
+  uint32_t a = s.h[0], b = s.h[1], c = s.h[2], d = s.h[3], e = s.h[4];
+#pragma unroll
+  for (int i = 0; i < 80; ++i) {
+    uint32_t x;
+    if (i < 16) {
+      x = w[i];
+    } else {
+      x = sched(w[(i + 13) & 15], w[(i + 8) & 15], w[(i + 2) & 15], w[i & 15]);
+      w[i & 15] = x;
+    }
+    uint32_t f, k;
+    if (i < 20) {
+      f = f_choose(b, c, d);
+      k = kK1;
+    } else if (i < 40) {
+      f = f_parity(b, c, d);
+      k = kK2;
+    } else if (i < 60) {
+      f = f_major(b, c, d);
+      k = kK3;
+    } else {
+      f = f_parity(b, c, d);
+      k = kK4;
+    }
+    const uint32_t t = rotl(a, 5) + f + e + (x + k);
+    e = d;
+    d = c;
+    c = rotl(b, 30);
+    b = a;
+    a = t;
+  }
+  s.h[0] += a;
+  s.h[1] += b;
+  s.h[2] += c;
+  s.h[3] += d;
+  s.h[4] += e;
+}
+
+// Big-endian block from four 16-byte little-endian vectors.
+__device__ __forceinline__ void block_from_vec(uint32_t (&w)[16], const uint4& q0, const uint4& q1,
+                                               const uint4& q2, const uint4& q3) {
+  w[0] = bswap(q0.x);  w[1] = bswap(q0.y);  w[2] = bswap(q0.z);  w[3] = bswap(q0.w);
+  w[4] = bswap(q1.x);  w[5] = bswap(q1.y);  w[6] = bswap(q1.z);  w[7] = bswap(q1.w);
+  w[8] = bswap(q2.x);  w[9] = bswap(q2.y);  w[10] = bswap(q2.z); w[11] = bswap(q2.w);
+  w[12] = bswap(q3.x); w[13] = bswap(q3.y); w[14] = bswap(q3.z); w[15] = bswap(q3.w);
+}
+
+// 64 bytes at any alignment as 16 little-endian words, for chunks whose start
+// is not 16-byte aligned and for the tail.  Only dwords that hold at least one
+// of the `valid` (>= 1) readable bytes are loaded -- an aligned dword never
+// straddles a page, so nothing past the chunk's last byte page is touched --
+// and v_alignbyte_b32 funnels them into place.  Words past `valid` hold
+// don't-care bytes the caller masks.
+__device__ __forceinline__ void load_words_any(uint32_t (&le)[16], const uint8_t* p, uint32_t valid) {
+  const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 3u);
+  const uint32_t* b = reinterpret_cast<const uint32_t*>(p - sh);
+  const uint32_t last = (sh + valid - 1) >> 2;  // last dword holding a valid byte (<= 16)
+  uint32_t d[17];
+#pragma unroll
+  for (uint32_t m = 0; m < 17; ++m) d[m] = b[m < last ? m : last];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) le[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+}
+
+// Final one or two blocks: the r = size % 64 trailing bytes, the 0x80 pad byte
+// and the big-endian bit length (iterhash.cpp:86-99, iterhash.h:106-121).
+__device__ __forceinline__ void finish(Digest& s, const uint8_t* tail, uint32_t r, uint32_t total) {
+  uint32_t w[16];
+  if (r) {
+    load_words_any(w, tail, r);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) w[k] = 0;
+  }
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int rem = (int)r - 4 * k;  // chunk bytes left in this word
+    uint32_t v = bswap(w[k]);
+    if (rem <= 0) v = 0;
+    if (rem >= 0 && rem < 4) {
+      const uint32_t sh = 8u * (uint32_t)rem;
+      v = (v & ~(0xFFFFFFFFu >> sh)) | (0x80000000u >> sh);  // keep `rem` bytes, then 0x80
+    }
+    w[k] = v;
+  }
+  const uint32_t nfinal = r >= 56 ? 2u : 1u;
+  for (uint32_t f = 0; f < nfinal; ++f) {
+    if (f + 1 == nfinal) {
+      w[14] = total >> 29;  // GetBitCountHi for a 32-bit byte count
+      w[15] = total << 3;   // GetBitCountLo
+    }
+    compress(s, w);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) w[k] = 0;  // second final block: zeros + length
+  }
+}
+
+// splitmix64 counter-mode synthetic stream; identical to
+// oracle_synth_word in oracle/sha1_oracle.c and synth_np in
+// tests/golden/make_golden.py.
+__device__ __forceinline__ uint64_t synth_word(uint64_t seed, uint64_t k) {
+  uint64_t z = seed * 0xD1B54A32D192ED03ull + (k + 1) * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+}  // namespace lbf

@@ -1,0 +1,198 @@
+"""Python face of the MI355X chunk-hash path (over liblbfhash.so).
+
+Mirrors the reference's hash entry points so tests read like the reference's
+own call sites:
+
+* ``base64_encode(data)`` == ``libBitFlood::Encoder::Base64Encode``
+  (/root/reference/cpp/src/Encoder.cpp:107-120): SHA-1 rendered as the
+  27-char unpadded base64 string.
+* ``ChunkHasher.hash_chunks`` == the per-chunk hash loop of
+  ``Encoder::EncodeFile`` (Encoder.cpp:54-72), batched.
+* ``ChunkHasher.verify_chunks`` == the compare-with-flood-file verify of
+  ``Flood::_SetupFilesAndChunks`` (Flood.cpp:259-275) and of
+  ``ChunkMethodHandler::_HandleSendChunk`` (ChunkMethods.cpp:165-167).
+
+All hashing runs on the GPU; there is no CPU path in this module.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _capi
+from ._capi import LBF_DEVICE_PTR, LBF_HOST_PTR, LbfError, check, load
+
+DIGEST = 20
+
+
+def b64_27(digest: bytes) -> str:
+    """20-byte digest -> 27-char string (basecode.cpp:39-104, no padding)."""
+    if len(digest) != DIGEST:
+        raise ValueError("digest must be 20 bytes")
+    out = ctypes.create_string_buffer(28)
+    load().lbf_b64_27(bytes(digest), out)
+    return out.value.decode()
+
+
+def b64_27_decode(s: str) -> bytes:
+    raw = s.encode()
+    out = (ctypes.c_uint8 * DIGEST)()
+    check(load().lbf_b64_27_decode(raw, len(raw), out))
+    return bytes(out)
+
+
+def chunk_table(length: int, chunk_size: int, base_offset: int = 0):
+    """Offsets/sizes of Encoder.cpp's fixed-size chunking of one file:
+    chunk i = [i*cs, min((i+1)*cs, length)); an empty file has no chunks."""
+    if chunk_size <= 0:
+        raise ValueError("chunk_size must be positive")
+    n = (length + chunk_size - 1) // chunk_size
+    offs = np.arange(n, dtype=np.uint64) * np.uint64(chunk_size)
+    sizes = np.full(n, chunk_size, dtype=np.uint32)
+    if n:
+        sizes[-1] = length - (n - 1) * chunk_size
+    return offs + np.uint64(base_offset), sizes
+
+
+def _as_u8(data) -> np.ndarray:
+    if isinstance(data, np.ndarray):
+        return np.ascontiguousarray(data).view(np.uint8).reshape(-1)
+    return np.frombuffer(memoryview(data), dtype=np.uint8)
+
+
+class ChunkHasher:
+    """An lbf_ctx: device buffers, streams and pinned staging on one or more GPUs."""
+
+    def __init__(self, device_mask: int = 0):
+        lib = load()
+        h = ctypes.c_void_p()
+        check(lib.lbf_ctx_create(device_mask, ctypes.byref(h)))
+        self._h = h
+        self._lib = lib
+
+    @property
+    def num_devices(self) -> int:
+        return self._lib.lbf_ctx_num_devices(self._h)
+
+    def close(self) -> None:
+        if self._h:
+            self._lib.lbf_ctx_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- host-memory batches -------------------------------------------------
+    def hash_chunks(self, data, offsets, sizes) -> np.ndarray:
+        buf = _as_u8(data)
+        offs = np.ascontiguousarray(offsets, dtype=np.uint64)
+        szs = np.ascontiguousarray(sizes, dtype=np.uint32)
+        if offs.shape != szs.shape:
+            raise ValueError("offsets and sizes differ in length")
+        n = offs.size
+        out = np.zeros((n, DIGEST), dtype=np.uint8)
+        if n == 0:
+            return out
+        base = buf.ctypes.data if buf.size else ctypes.addressof(ctypes.c_uint8(0))
+        check(self._lib.lbf_sha1_batch(self._h, base, buf.size, offs.ctypes.data, szs.ctypes.data, n,
+                                       out.ctypes.data, LBF_HOST_PTR))
+        return out
+
+    def verify_chunks(self, data, offsets, sizes, expected) -> np.ndarray:
+        buf = _as_u8(data)
+        offs = np.ascontiguousarray(offsets, dtype=np.uint64)
+        szs = np.ascontiguousarray(sizes, dtype=np.uint32)
+        exp = np.ascontiguousarray(expected, dtype=np.uint8).reshape(-1, DIGEST)
+        n = offs.size
+        if szs.size != n or exp.shape[0] != n:
+            raise ValueError("offsets, sizes and expected differ in length")
+        ver = np.zeros(n, dtype=np.uint8)
+        if n == 0:
+            return ver.astype(bool)
+        base = buf.ctypes.data if buf.size else ctypes.addressof(ctypes.c_uint8(0))
+        check(self._lib.lbf_verify_batch(self._h, base, buf.size, offs.ctypes.data, szs.ctypes.data, n,
+                                         exp.ctypes.data, ver.ctypes.data, LBF_HOST_PTR))
+        return ver.astype(bool)
+
+    def sha1(self, data) -> bytes:
+        buf = _as_u8(data)
+        out = (ctypes.c_uint8 * DIGEST)()
+        base = buf.ctypes.data if buf.size else None
+        check(self._lib.lbf_sha1_one(self._h, base, buf.size, out))
+        return bytes(out)
+
+    def base64_encode(self, data) -> str:
+        """Encoder::Base64Encode(data, size, out) (Encoder.cpp:107-120)."""
+        return b64_27(self.sha1(data))
+
+    def encode_buffer(self, data, chunk_size: int) -> list[str]:
+        """Per-chunk hash strings of one in-memory file (Encoder.cpp:54-72)."""
+        buf = _as_u8(data)
+        offs, sizes = chunk_table(buf.size, chunk_size)
+        return [b64_27(bytes(d)) for d in self.hash_chunks(buf, offs, sizes)]
+
+
+# ---------------------------------------------------------------------------
+# Device-resident helpers (bench.py, parity tests at full size)
+# ---------------------------------------------------------------------------
+class DeviceBuffer:
+    def __init__(self, nbytes: int):
+        self.nbytes = int(nbytes)
+        p = ctypes.c_void_p()
+        check(load().lbf_dev_malloc(ctypes.byref(p), self.nbytes))
+        self.ptr = p.value
+
+    def free(self):
+        if self.ptr:
+            check(load().lbf_dev_free(self.ptr))
+            self.ptr = None
+
+    def upload(self, host: np.ndarray, offset: int = 0):
+        host = np.ascontiguousarray(host)
+        check(load().lbf_memcpy_h2d(self.ptr + offset, host.ctypes.data, host.nbytes))
+
+    def download(self, nbytes: int | None = None, offset: int = 0, dtype=np.uint8) -> np.ndarray:
+        nbytes = self.nbytes - offset if nbytes is None else nbytes
+        out = np.empty(nbytes, dtype=np.uint8)
+        check(load().lbf_memcpy_d2h(out.ctypes.data, self.ptr + offset, nbytes))
+        return out.view(dtype)
+
+    def fill_synthetic(self, seed: int, start: int = 0, nbytes: int | None = None, stream=None):
+        nbytes = self.nbytes if nbytes is None else nbytes
+        check(load().lbf_fill_synthetic(self.ptr, nbytes, seed, start, stream))
+
+
+def uniform_launch(base: DeviceBuffer | int, length: int, chunk_size: int, first: int, n: int,
+                   digests: DeviceBuffer | int | None, expected=None, verdicts=None, stream=None):
+    p = lambda x: None if x is None else (x.ptr if isinstance(x, DeviceBuffer) else x)  # noqa: E731
+    check(load().lbf_sha1_uniform_launch(p(base), length, chunk_size, first, n, p(digests), p(expected),
+                                         p(verdicts), stream))
+
+
+def batch_launch(base, offsets, sizes, n, digests, expected=None, verdicts=None, stream=None):
+    p = lambda x: None if x is None else (x.ptr if isinstance(x, DeviceBuffer) else x)  # noqa: E731
+    check(load().lbf_sha1_launch(p(base), p(offsets), p(sizes), n, p(digests), p(expected), p(verdicts),
+                                 stream))
+
+
+def synchronize():
+    check(load().lbf_device_synchronize())
+
+
+def set_kernel_variant(v: int):
+    check(load().lbf_set_kernel_variant(v))
+
+
+__all__ = ["ChunkHasher", "DeviceBuffer", "LbfError", "b64_27", "b64_27_decode", "chunk_table",
+           "uniform_launch", "batch_launch", "synchronize", "set_kernel_variant", "LBF_DEVICE_PTR",
+           "_capi"]

@@ -1,0 +1,140 @@
+/*
+ * lbf_hash.h -- C ABI of the MI355X chunk-hash path for bitflood.
+ *
+ * This is the drop-in boundary beneath the reference's C++ entry points
+ *   Error::ErrorCode libBitFlood::Encoder::Base64Encode(const U8*, U32, std::string&)
+ *       (/root/reference/cpp/src/Encoder.H:28, Encoder.cpp:107-120)
+ *   Error::ErrorCode libBitFlood::Encoder::EncodeFile(const ToEncode&, FloodFile&)
+ *       (/root/reference/cpp/src/Encoder.H:27, Encoder.cpp:17-102)
+ * and beneath the verify call sites that compare a chunk's hash with the
+ * flood-file string
+ *   Flood::_SetupFilesAndChunks      (/root/reference/cpp/src/Flood.cpp:259-275)
+ *   ChunkMethodHandler::_HandleRequestChunk (/root/reference/cpp/src/ChunkMethods.cpp:116-123)
+ *   ChunkMethodHandler::_HandleSendChunk    (/root/reference/cpp/src/ChunkMethods.cpp:165-167)
+ * The C++ wrappers with the reference's exact signatures live in
+ * include/libBitFlood/ (libbitflood.so); they call only what is declared here.
+ *
+ * Conventions (C convention, unlike the reference's ErrorCode where 1 = ok):
+ *   - every int-returning call returns LBF_OK (0) on success or a negative
+ *     lbf_status; lbf_last_error() returns a thread-local message;
+ *   - the caller owns every host array; a context owns device memory,
+ *     streams and pinned staging;
+ *   - digests are raw 20-byte SHA-1 (big-endian word order, as the reference's
+ *     HashFilter emits them, iterhash.h:117-118); chunk i's digest is at
+ *     out_digests + 20*i;
+ *   - nothing is thrown across the ABI.
+ */
+#ifndef LBF_HASH_H_
+#define LBF_HASH_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LBF_ABI_VERSION 1
+#define LBF_DIGEST_BYTES 20
+#define LBF_B64_CHARS 27
+
+typedef enum lbf_status {
+  LBF_OK = 0,
+  LBF_ERR_INVALID = -1,   /* bad argument (null pointer, size overflow, ...) */
+  LBF_ERR_NO_DEVICE = -2, /* no MI355X visible: the path has no CPU fallback */
+  LBF_ERR_HIP = -3,       /* HIP runtime or kernel launch failure */
+  LBF_ERR_NOMEM = -4,     /* device or pinned host allocation failed */
+  LBF_ERR_IO = -5         /* file could not be opened / read */
+} lbf_status;
+
+/* `flags` for the batch calls: where `base`, `offsets`, `sizes`, `expected`
+ * and the outputs live. */
+#define LBF_HOST_PTR 0
+#define LBF_DEVICE_PTR 1
+
+typedef struct lbf_ctx lbf_ctx;
+
+/* ---- library / context ------------------------------------------------- */
+int lbf_abi_version(void);
+const char* lbf_last_error(void);
+/* Number of visible GPUs (0 when none; never an error on a CPU-only host). */
+int lbf_device_count(int* out_count);
+/* device_mask bit d selects device d; 0 selects every visible device.
+ * Fails with LBF_ERR_NO_DEVICE when no GPU is visible. */
+int lbf_ctx_create(uint32_t device_mask, lbf_ctx** out_ctx);
+void lbf_ctx_destroy(lbf_ctx* ctx);
+int lbf_ctx_num_devices(const lbf_ctx* ctx);
+
+/* ---- batched chunk hashing (Encoder::EncodeFile's per-chunk hash) --------
+ * Chunk i is the byte range [offsets[i], offsets[i] + sizes[i]) of `base`.
+ * LBF_HOST_PTR: base/offsets/sizes/out are host memory; `base_len` bounds
+ *   the readable range of `base`.  Chunks are streamed through pinned staging
+ *   to the context's devices (contiguous index ranges per device).
+ * LBF_DEVICE_PTR: everything is device memory of the context's first device
+ *   and the call is synchronous on the context stream. */
+int lbf_sha1_batch(lbf_ctx* ctx, const uint8_t* base, uint64_t base_len,
+                   const uint64_t* offsets, const uint32_t* sizes, uint64_t n,
+                   uint8_t* out_digests, int flags);
+
+/* ---- batched verify (Flood.cpp:259-275, ChunkMethods.cpp:116-123,165-167)
+ * verdicts[i] = 1 when SHA-1(chunk i) equals expected[20*i .. 20*i+20),
+ * else 0.  The comparison happens on the device. */
+int lbf_verify_batch(lbf_ctx* ctx, const uint8_t* base, uint64_t base_len,
+                     const uint64_t* offsets, const uint32_t* sizes, uint64_t n,
+                     const uint8_t* expected, uint8_t* verdicts, int flags);
+
+/* ---- single buffer (Encoder::Base64Encode's hash, host memory) ---------- */
+int lbf_sha1_one(lbf_ctx* ctx, const uint8_t* data, uint32_t size, uint8_t out_digest[20]);
+
+/* ---- digest <-> 27-char string (basecode.cpp:39-104, Encoder.cpp:104-105)
+ * lbf_b64_27 writes 27 chars + NUL.  lbf_b64_27_decode accepts exactly 27
+ * chars of the standard alphabet whose last char carries 4 data bits and 2
+ * zero bits; anything else returns LBF_ERR_INVALID. */
+void lbf_b64_27(const uint8_t digest[20], char out[28]);
+int lbf_b64_27_decode(const char* in, size_t len, uint8_t out_digest[20]);
+
+/* ---- device-resident asynchronous entry points ---------------------------
+ * All pointers are device memory on the current HIP device; `stream` is a
+ * hipStream_t (NULL = the default stream).  These enqueue and return; they
+ * are what bench.py times and what the pipelined host paths use.
+ * d_expected/d_verdicts may be NULL (hash only); d_digests may be NULL when
+ * only verdicts are wanted. */
+int lbf_sha1_launch(const uint8_t* d_base, const uint64_t* d_offsets,
+                    const uint32_t* d_sizes, uint64_t n, uint8_t* d_digests,
+                    const uint8_t* d_expected, uint8_t* d_verdicts, void* stream);
+/* Uniform chunking of one region (one file laid out contiguously):
+ * chunk i = [i*chunk_size, min((i+1)*chunk_size, len)), i in [first, first+n). */
+int lbf_sha1_uniform_launch(const uint8_t* d_base, uint64_t len, uint32_t chunk_size,
+                            uint64_t first_chunk, uint64_t n, uint8_t* d_digests,
+                            const uint8_t* d_expected, uint8_t* d_verdicts, void* stream);
+/* Kernel variant selection for the two launchers above (0 = automatic).
+ * Exposed for benchmarking and tests; see DESIGN.md "kernels". */
+int lbf_set_kernel_variant(int variant);
+int lbf_get_kernel_variant(void);
+
+/* Synthetic bytes (counter-mode splitmix64): fill
+ * d_buf[0..len) with stream `seed` starting at stream byte `start`
+ * (start % 8 == 0, d_buf 16-byte aligned). */
+int lbf_fill_synthetic(uint8_t* d_buf, uint64_t len, uint64_t seed, uint64_t start, void* stream);
+
+/* Tiny device-memory helpers so C/ctypes callers need no HIP headers. */
+int lbf_dev_malloc(void** out_ptr, uint64_t bytes);
+int lbf_dev_free(void* ptr);
+int lbf_memcpy_h2d(void* dst, const void* src, uint64_t bytes);
+int lbf_memcpy_d2h(void* dst, const void* src, uint64_t bytes);
+int lbf_set_device(int device);
+int lbf_device_synchronize(void);
+int lbf_stream_create(void** out_stream);
+int lbf_stream_destroy(void* stream);
+int lbf_stream_synchronize(void* stream);
+/* Time `reps` back-to-back launches of lbf_sha1_uniform_launch on `stream`
+ * with HIP events recorded on that stream; writes the mean ms per launch. */
+int lbf_time_uniform(const uint8_t* d_base, uint64_t len, uint32_t chunk_size,
+                     uint64_t first_chunk, uint64_t n, uint8_t* d_digests, int reps,
+                     void* stream, float* out_ms_per_launch);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* LBF_HASH_H_ */

@@ -1,0 +1,69 @@
+"""The C-ABI library loads and exports every symbol include/lbf_hash.h declares.
+
+CPU-only checks: no hashing happens here (there is no CPU hashing path); the
+GPU-less behaviour tested is that the context refuses to start loudly.
+"""
+import base64
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from bitflood_amd import _capi
+
+
+def test_library_exports_every_header_symbol():
+    lib = _capi.load()
+    syms = _capi.header_symbols()
+    assert "lbf_sha1_batch" in syms and "lbf_verify_batch" in syms and "lbf_b64_27" in syms
+    missing = [s for s in syms if not hasattr(lib, s)]
+    assert not missing, missing
+    # and the binding covers the whole header
+    assert sorted(_capi._SIGS) == syms
+
+
+def test_exported_symbols_are_c_linkage():
+    out = subprocess.run(["nm", "-D", "--defined-only", _capi.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    names = {line.split()[-1] for line in out.splitlines() if line.strip()}
+    for s in _capi.header_symbols():
+        assert s in names, f"{s} not exported with C linkage"
+
+
+def test_abi_version():
+    assert _capi.load().lbf_abi_version() == 1
+
+
+def test_b64_27_host_formatting_matches_python():
+    from bitflood_amd import b64_27, b64_27_decode
+    rng = np.random.default_rng(5)
+    for _ in range(100):
+        d = rng.integers(0, 256, 20, dtype=np.uint8).tobytes()
+        s = b64_27(d)
+        assert s == base64.b64encode(d).decode().rstrip("=")
+        assert b64_27_decode(s) == d
+
+
+def test_b64_27_decode_rejects_malformed():
+    from bitflood_amd import LbfError, b64_27_decode
+    good = "qZk+NkcGgWq6PiVxeFDCbJzQ2J0"
+    assert b64_27_decode(good).hex() == "a9993e364706816aba3e25717850c26c9cd0d89d"
+    for bad in [good[:-1], good + "A", good[:-1] + "1", good[:5] + "*" + good[6:], ""]:
+        with pytest.raises(LbfError):
+            b64_27_decode(bad)
+
+
+@pytest.mark.skipif(_capi.device_count() > 0, reason="only meaningful without a GPU")
+def test_no_gpu_fails_loudly():
+    from bitflood_amd import ChunkHasher, LbfError
+    with pytest.raises(LbfError) as ei:
+        ChunkHasher()
+    assert ei.value.status == _capi.LBF_ERR_NO_DEVICE
+    assert "no CPU fallback" in str(ei.value)
+
+
+def test_kernels_compiled_for_gfx950():
+    blob = open(_capi.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob

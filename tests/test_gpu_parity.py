@@ -1,0 +1,201 @@
+"""Parity of the MI355X chunk-hash kernels against the oracle and the golden fixtures.
+
+Bit-exact: SHA-1 digests are integer/byte results, so every comparison is
+equality.  Small cases go through the oracle (oracle/sha1_oracle.c) on the same
+seeded bytes; full-size C2 (4 GiB at 256 KiB chunks) is checked through
+size-independent properties against hashlib goldens: the SHA-1 of the 16,384
+concatenated raw digests, sampled chunk strings, and a verify round trip.
+"""
+import hashlib
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from bitflood_amd import ChunkHasher, DeviceBuffer, b64_27, chunk_table
+from bitflood_amd import hashing as H
+
+pytestmark = pytest.mark.gpu
+SEED_C = 0x5EED
+
+
+def _kat_message(k):
+    if k["text"] is not None:
+        return k["text"].encode()
+    if k["name"] == "a_x_1e6":
+        return b"a" * k["len"]
+    return bytes(k["len"])
+
+
+def test_kats(hasher, golden):
+    for k in golden("kat.json")["kats"]:
+        m = _kat_message(k)
+        assert hasher.sha1(m).hex() == k["hex"], k["name"]
+        assert hasher.base64_encode(m) == k["b64_27"], k["name"]
+
+
+def test_tails(hasher, oracle, golden):
+    for t in golden("synthetic.json")["tails"]:
+        data = oracle.synth(t["seed"], 0, t["size"])
+        assert hasher.encode_buffer(data, t["chunk_size"]) == t["b64"], (t["size"], t["chunk_size"])
+
+
+def test_ragged_misaligned(hasher, oracle, golden):
+    r = golden("synthetic.json")["ragged"]
+    buf = oracle.synth(r["seed"], 0, r["buf_len"])
+    got = hasher.hash_chunks(buf, r["offsets"], r["sizes"])
+    assert [bytes(d).hex() for d in got] == r["hex"]
+
+
+def test_random_batch_vs_oracle(hasher, oracle):
+    rng = np.random.default_rng(11)
+    buf = oracle.synth(12, 0, 24 << 20)
+    n = 3000
+    sizes = rng.integers(0, 70000, n).astype(np.uint32)
+    sizes[:40] = np.arange(40) * 3  # tiny, every residue class around 0..117
+    offs = np.array([rng.integers(0, buf.size - s + 1) for s in sizes], dtype=np.uint64)
+    offs[::2] &= ~np.uint64(63)  # half aligned, half anywhere
+    got = hasher.hash_chunks(buf, offs, sizes)
+    want = oracle.sha1_batch(buf, offs, sizes, nthreads=os.cpu_count() or 1)
+    bad = np.nonzero((got != want).any(axis=1))[0]
+    assert bad.size == 0, f"{bad.size} mismatches, first at {bad[:5]} sizes {sizes[bad[:5]]}"
+
+
+def test_empty_inputs(hasher):
+    assert hasher.sha1(b"").hex() == "da39a3ee5e6b4b0d3255bfef95601890afd80709"
+    out = hasher.hash_chunks(np.zeros(16, np.uint8), np.zeros(0, np.uint64), np.zeros(0, np.uint32))
+    assert out.shape == (0, 20)
+    # zero-size chunk anywhere in a batch
+    d = hasher.hash_chunks(np.arange(100, dtype=np.uint8), [0, 100, 5], [0, 0, 1])
+    assert bytes(d[0]) == bytes(d[1]) == hashlib.sha1(b"").digest()
+    assert bytes(d[2]) == hashlib.sha1(bytes([5])).digest()
+
+
+def test_c1(hasher, oracle, golden):
+    c1 = golden("c1.json")
+    data = oracle.synth(c1["seed"], 0, c1["size"])
+    assert hasher.encode_buffer(data, c1["chunk_size"]) == c1["b64"]
+    o = c1["odd_tail"]
+    data = oracle.synth(o["seed"], 0, o["size"])
+    assert hasher.encode_buffer(data, o["chunk_size"]) == o["b64"]
+
+
+def test_verify_round_trip(hasher, oracle):
+    data = oracle.synth(21, 0, 8 << 20)
+    offs, sizes = chunk_table(data.size, 65536)
+    exp = hasher.hash_chunks(data, offs, sizes)
+    assert hasher.verify_chunks(data, offs, sizes, exp).all()
+    bad_data = data.copy()
+    for idx in [0, 17, 127]:
+        bad_data[idx * 65536 + 1000] ^= 0x40
+    v = hasher.verify_chunks(bad_data, offs, sizes, exp)
+    assert np.nonzero(~v)[0].tolist() == [0, 17, 127]
+    exp2 = exp.copy()
+    exp2[5, 19] ^= 1
+    v = hasher.verify_chunks(data, offs, sizes, exp2)
+    assert np.nonzero(~v)[0].tolist() == [5]
+
+
+def test_small_slots_and_oversize_chunks(oracle):
+    """Force many staging groups (1 MiB slots) and the oversize-chunk path."""
+    os.environ["LBF_SLOT_MB"] = "1"
+    try:
+        h = ChunkHasher()
+    finally:
+        del os.environ["LBF_SLOT_MB"]
+    try:
+        data = oracle.synth(31, 0, 9 << 20)
+        offs = np.array([0, 3, 1 << 20, (1 << 20) + 7, 5 << 20, 100], dtype=np.uint64)
+        sizes = np.array([1 << 20, (1 << 20) - 3, (3 << 20) + 5, 65, 4 << 20, 1], dtype=np.uint32)
+        got = h.hash_chunks(data, offs, sizes)
+        want = oracle.sha1_batch(data, offs, sizes)
+        assert np.array_equal(got, want)
+        offs, sizes = chunk_table(data.size, 300001)
+        assert np.array_equal(h.hash_chunks(data, offs, sizes), oracle.sha1_batch(data, offs, sizes))
+    finally:
+        h.close()
+
+
+def test_device_fill_matches_oracle_stream(oracle):
+    buf = DeviceBuffer(1 << 20)
+    try:
+        buf.fill_synthetic(SEED_C, start=1 << 30)
+        got = buf.download()
+        assert np.array_equal(got, oracle.synth(SEED_C, 1 << 30, 1 << 20))
+        buf.fill_synthetic(7, start=16, nbytes=1001)
+        got = buf.download(1001)
+        assert np.array_equal(got, oracle.synth(7, 16, 1001))
+    finally:
+        buf.free()
+
+
+def test_device_ptr_batch(hasher, oracle):
+    from bitflood_amd import _capi
+    data = oracle.synth(41, 0, 1 << 20)
+    offs = np.array([0, 64, 129, 4096, 70000], dtype=np.uint64)
+    sizes = np.array([64, 65, 1000, 60000, 300000], dtype=np.uint32)
+    d_data, d_off, d_size, d_out = (DeviceBuffer(data.size), DeviceBuffer(40), DeviceBuffer(20),
+                                    DeviceBuffer(100))
+    try:
+        d_data.upload(data)
+        d_off.upload(offs)
+        d_size.upload(sizes)
+        _capi.check(_capi.load().lbf_sha1_batch(hasher._h, d_data.ptr, data.size, d_off.ptr, d_size.ptr, 5,
+                                                d_out.ptr, _capi.LBF_DEVICE_PTR))
+        got = d_out.download(100).reshape(5, 20)
+        assert np.array_equal(got, oracle.sha1_batch(data, offs, sizes))
+    finally:
+        for b in (d_data, d_off, d_size, d_out):
+            b.free()
+
+
+def test_uniform_partial_last_chunk(oracle):
+    n_bytes = (5 << 20) + 12345
+    buf = DeviceBuffer(n_bytes)
+    dig = DeviceBuffer(21 * 20)
+    try:
+        buf.fill_synthetic(77)
+        n = (n_bytes + 262143) // 262144
+        H.uniform_launch(buf, n_bytes, 262144, 0, n, dig)
+        H.synchronize()
+        got = dig.download(n * 20).reshape(n, 20)
+        want = oracle.encode_buffer(oracle.synth(77, 0, n_bytes), 262144)
+        assert np.array_equal(got, want)
+        # sub-range launch (first_chunk > 0) as a sharded rank would issue it
+        H.uniform_launch(buf, n_bytes, 262144, 7, n - 7, dig)
+        H.synchronize()
+        assert np.array_equal(dig.download((n - 7) * 20).reshape(n - 7, 20), want[7:])
+    finally:
+        buf.free()
+        dig.free()
+
+
+def test_c2_full_size_device_resident(golden, oracle):
+    """C2: one 4 GiB file, 256 KiB chunks, entirely in HBM."""
+    c2 = golden("c2.json")
+    size, cs, n = c2["size"], c2["chunk_size"], c2["n_chunks"]
+    buf = DeviceBuffer(size)
+    dig = DeviceBuffer(n * 20)
+    ver = DeviceBuffer(n)
+    try:
+        buf.fill_synthetic(c2["seed"])
+        H.uniform_launch(buf, size, cs, 0, n, dig)
+        H.synchronize()
+        d = dig.download(n * 20).reshape(n, 20)
+        assert hashlib.sha1(d.tobytes()).hexdigest() == c2["sha1_of_concat_raw_digests_hex"]
+        for k, v in c2["samples_b64"].items():
+            assert b64_27(bytes(d[int(k)])) == v
+        # spot-check against the oracle on device-generated bytes
+        for i in [5, 9000]:
+            chunk = buf.download(cs, offset=i * cs)
+            assert oracle.sha1(chunk) == bytes(d[i])
+        # verify mode against the just-computed digests: every verdict 1
+        H.uniform_launch(buf, size, cs, 0, n, None, expected=dig, verdicts=ver)
+        H.synchronize()
+        assert ver.download(n).all()
+    finally:
+        buf.free()
+        dig.free()
+        ver.free()

@@ -1,0 +1,132 @@
+"""Pin the CPU oracle (oracle/sha1_oracle.c) before trusting it as the checker.
+
+Anchors: Crypto++ SHA-1 KATs (cpp/extern/crypto++/5.2.1/TestVectors/sha.txt:1-11),
+hashlib-generated golden fixtures (tests/golden/make_golden.py), and Python's
+base64 for the 27-char rendering (basecode.cpp:39-104 without padding).
+"""
+import base64
+import hashlib
+import os
+
+import numpy as np
+import pytest
+
+SEED_C = 0x5EED
+
+
+def _kat_message(k):
+    if k["text"] is not None:
+        return k["text"].encode()
+    if k["name"] == "a_x_1e6":
+        return b"a" * k["len"]
+    return bytes(k["len"])
+
+
+def test_kats(oracle, golden):
+    for k in golden("kat.json")["kats"]:
+        m = _kat_message(k)
+        d = oracle.sha1(m)
+        assert d.hex() == k["hex"], k["name"]
+        assert oracle.base64_encode(m) == k["b64_27"], k["name"]
+
+
+def test_crypto_pp_kat_hex_column(golden):
+    # sha.txt:3-10 / validat3.cpp:171-176 digests, verbatim upper-case hex
+    ref = {"abc": "A9993E364706816ABA3E25717850C26C9CD0D89D",
+           "nist448": "84983E441C3BD26EBAAE4AA1F95129E5E54670F1",
+           "a_x_1e6": "34AA973CD4C4DAA4F61EEB2BDBAD27316534016F"}
+    got = {k["name"]: k["hex"].upper() for k in golden("kat.json")["kats"]}
+    for name, hexd in ref.items():
+        assert got[name] == hexd
+
+
+def test_incremental_update_matches_one_shot(oracle):
+    """iterhash.cpp:9-63 left-over handling: any split of Update calls gives the same digest."""
+    rng = np.random.default_rng(1)
+    for n in [0, 1, 55, 56, 63, 64, 65, 127, 128, 129, 1000, 4097]:
+        data = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        want = hashlib.sha1(data).digest()
+        assert oracle.sha1(data) == want
+        for _ in range(3):
+            splits = sorted(rng.integers(0, n + 1, size=int(rng.integers(0, 6))).tolist())
+            assert oracle.sha1_incremental(data, splits) == want
+
+
+def test_b64_27_restatement(oracle):
+    rng = np.random.default_rng(2)
+    for _ in range(200):
+        d = rng.integers(0, 256, 20, dtype=np.uint8).tobytes()
+        want = base64.b64encode(d).decode().rstrip("=")
+        assert oracle.b64_27(d) == want
+        assert len(want) == 27
+
+
+def test_synthetic_stream_probe(oracle, golden):
+    sp = golden("synthetic.json")["stream_probe"]
+    assert oracle.synth(SEED_C, 0, 32).tobytes().hex() == sp["first32_hex"]
+    assert oracle.synth(SEED_C, 1 << 30, 32).tobytes().hex() == sp["at_1GiB_hex"]
+    assert oracle.synth(7, 13, 19).tobytes().hex() == sp["seed7_off13_hex"]
+    a = oracle.synth(99, 5, 100003, nthreads=1)
+    b = oracle.synth(99, 5, 100003, nthreads=4)
+    assert np.array_equal(a, b)
+
+
+def test_tails_golden(oracle, golden):
+    for t in golden("synthetic.json")["tails"]:
+        data = oracle.synth(t["seed"], 0, t["size"])
+        got = [oracle.b64_27(bytes(d)) for d in oracle.encode_buffer(data, t["chunk_size"])]
+        assert got == t["b64"], (t["size"], t["chunk_size"])
+
+
+def test_ragged_golden(oracle, golden):
+    r = golden("synthetic.json")["ragged"]
+    buf = oracle.synth(r["seed"], 0, r["buf_len"])
+    got = oracle.sha1_batch(buf, r["offsets"], r["sizes"], nthreads=4)
+    assert [bytes(d).hex() for d in got] == r["hex"]
+
+
+def test_c1_golden(oracle, golden):
+    c1 = golden("c1.json")
+    data = oracle.synth(c1["seed"], 0, c1["size"])
+    got = [oracle.b64_27(bytes(d)) for d in oracle.encode_buffer(data, c1["chunk_size"])]
+    assert len(got) == 256
+    assert got == c1["b64"]
+    o = c1["odd_tail"]
+    data = oracle.synth(o["seed"], 0, o["size"])
+    got = [oracle.b64_27(bytes(d)) for d in oracle.encode_buffer(data, o["chunk_size"])]
+    assert got == o["b64"]
+
+
+def test_encode_file_fread_path(oracle, tmp_path):
+    """Encoder.cpp:40-79 restated with fread: empty file -> 0 chunks, short tail kept."""
+    p = tmp_path / "f.bin"
+    data = oracle.synth(3, 0, 3 * 4096 + 17)
+    p.write_bytes(data.tobytes())
+    out = np.zeros((8, 20), dtype=np.uint8)
+    sizes = np.zeros(8, dtype=np.uint32)
+    n = oracle.lib.oracle_encode_file(str(p).encode(), 4096, out.ctypes.data, 8, sizes.ctypes.data)
+    assert n == 4
+    assert sizes[:4].tolist() == [4096, 4096, 4096, 17]
+    for i in range(4):
+        assert bytes(out[i]) == hashlib.sha1(data[i * 4096:(i + 1) * 4096].tobytes()).digest()
+    e = tmp_path / "empty.bin"
+    e.write_bytes(b"")
+    assert oracle.lib.oracle_encode_file(str(e).encode(), 4096, out.ctypes.data, 8, None) == 0
+    assert oracle.lib.oracle_encode_file(str(tmp_path / "missing").encode(), 4096, out.ctypes.data, 8, None) == -1
+
+
+@pytest.mark.slow
+def test_c2_digest_of_digests(oracle, golden):
+    """Full C2 (4 GiB, 256 KiB chunks) through the oracle, multithreaded: the
+    SHA-1 of the 16,384 concatenated raw digests equals the hashlib golden."""
+    c2 = golden("c2.json")
+    nt = os.cpu_count() or 1
+    data = oracle.synth(c2["seed"], 0, c2["size"], nthreads=nt)
+    n = c2["n_chunks"]
+    offs = np.arange(n, dtype=np.uint64) * np.uint64(c2["chunk_size"])
+    sizes = np.full(n, c2["chunk_size"], dtype=np.uint32)
+    d = oracle.sha1_batch(data, offs, sizes, nthreads=nt)
+    del data
+    assert hashlib.sha1(d.tobytes()).hexdigest() == c2["sha1_of_concat_raw_digests_hex"]
+    for k, v in c2["samples_b64"].items():
+        assert oracle.b64_27(bytes(d[int(k)])) == v
