@@ -65,6 +65,33 @@ struct Digest {
   }
 };
 
+// One SHA-1 round (sha.cpp:34-38) with round index i known at compile time
+// after unrolling.  `x` is the schedule word W[i].  The five-term sum is two
+// v_add3_u32 (the round constant rides in an SGPR/literal).
+__device__ __forceinline__ void round_step(int i, uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d,
+                                           uint32_t& e, uint32_t x) {
+  uint32_t f, k;
+  if (i < 20) {
+    f = f_choose(b, c, d);
+    k = kK1;
+  } else if (i < 40) {
+    f = f_parity(b, c, d);
+    k = kK2;
+  } else if (i < 60) {
+    f = f_major(b, c, d);
+    k = kK3;
+  } else {
+    f = f_parity(b, c, d);
+    k = kK4;
+  }
+  const uint32_t t = rotl(a, 5) + f + (e + x + k);
+  e = d;
+  d = c;
+  c = rotl(b, 30);
+  b = a;
+  a = t;
+}
+
 // One compression of a 16-word big-endian block.  `w` is consumed as the
 // 16-word rolling message schedule (the blk1 window of sha.cpp:15).
 __device__ __forceinline__ void compress(Digest& s, uint32_t (&w)[16]) {
@@ -78,32 +105,50 @@ __device__ __forceinline__ void compress(Digest& s, uint32_t (&w)[16]) {
       x = sched(w[(i + 13) & 15], w[(i + 8) & 15], w[(i + 2) & 15], w[i & 15]);
       w[i & 15] = x;
     }
-    uint32_t f, k;
-    if (i < 20) {
-      f = f_choose(b, c, d);
-      k = kK1;
-    } else if (i < 40) {
-      f = f_parity(b, c, d);
-      k = kK2;
-    } else if (i < 60) {
-      f = f_major(b, c, d);
-      k = kK3;
-    } else {
-      f = f_parity(b, c, d);
-      k = kK4;
-    }
-    const uint32_t t = rotl(a, 5) + f + e + (x + k);
-    e = d;
-    d = c;
-    c = rotl(b, 30);
-    b = a;
-    a = t;
+    round_step(i, a, b, c, d, e, x);
   }
   s.h[0] += a;
   s.h[1] += b;
   s.h[2] += c;
   s.h[3] += d;
   s.h[4] += e;
+}
+
+// Compression with the 80-word schedule already expanded (by a producer wave)
+// and stored in LDS as 20 uint4 per chain, `stride` uint4 apart.
+__device__ __forceinline__ void compress_expanded(Digest& s, const uint4* w, int stride) {
+  uint32_t a = s.h[0], b = s.h[1], c = s.h[2], d = s.h[3], e = s.h[4];
+#pragma unroll
+  for (int q = 0; q < 20; ++q) {
+    const uint4 v = w[q * stride];
+    round_step(4 * q + 0, a, b, c, d, e, v.x);
+    round_step(4 * q + 1, a, b, c, d, e, v.y);
+    round_step(4 * q + 2, a, b, c, d, e, v.z);
+    round_step(4 * q + 3, a, b, c, d, e, v.w);
+  }
+  s.h[0] += a;
+  s.h[1] += b;
+  s.h[2] += c;
+  s.h[3] += d;
+  s.h[4] += e;
+}
+
+// Expand a 16-word block into the 80-word schedule and store it as 20 uint4
+// (`stride` uint4 apart): the producer half of compress_expanded.
+__device__ __forceinline__ void expand_store(uint32_t (&w)[16], uint4* out, int stride) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) out[q * stride] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+#pragma unroll
+  for (int q = 4; q < 20; ++q) {
+    uint32_t x[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = 4 * q + j;
+      x[j] = sched(w[(i + 13) & 15], w[(i + 8) & 15], w[(i + 2) & 15], w[i & 15]);
+      w[i & 15] = x[j];
+    }
+    out[q * stride] = make_uint4(x[0], x[1], x[2], x[3]);
+  }
 }
 
 // Big-endian block from four 16-byte little-endian vectors.
@@ -132,37 +177,50 @@ __device__ __forceinline__ void load_words_any(uint32_t (&le)[16], const uint8_t
   for (int k = 0; k < 16; ++k) le[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
 }
 
-// Final one or two blocks: the r = size % 64 trailing bytes, the 0x80 pad byte
-// and the big-endian bit length (iterhash.cpp:86-99, iterhash.h:106-121).
-__device__ __forceinline__ void finish(Digest& s, const uint8_t* tail, uint32_t r, uint32_t total) {
-  uint32_t w[16];
-  if (r) {
+// Final-block words: the r = size % 64 trailing bytes, the 0x80 pad byte and
+// (when `with_len`) the big-endian bit length (iterhash.cpp:86-99,
+// iterhash.h:30-31,106-121).  `which` = 0 builds the block holding the tail
+// bytes; 1 builds the all-zero second block used when r >= 56.
+__device__ __forceinline__ void final_block(uint32_t (&w)[16], const uint8_t* tail, uint32_t r, uint32_t total,
+                                            bool second) {
+  if (r && !second) {
     load_words_any(w, tail, r);
   } else {
 #pragma unroll
     for (int k = 0; k < 16; ++k) w[k] = 0;
   }
+  const uint32_t rr = second ? 0u : r;
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
-    const int rem = (int)r - 4 * k;  // chunk bytes left in this word
+    const int rem = (int)rr - 4 * k;  // chunk bytes left in this word
     uint32_t v = bswap(w[k]);
     if (rem <= 0) v = 0;
-    if (rem >= 0 && rem < 4) {
+    if (!second && rem >= 0 && rem < 4) {
       const uint32_t sh = 8u * (uint32_t)rem;
       v = (v & ~(0xFFFFFFFFu >> sh)) | (0x80000000u >> sh);  // keep `rem` bytes, then 0x80
     }
     w[k] = v;
   }
-  const uint32_t nfinal = r >= 56 ? 2u : 1u;
-  for (uint32_t f = 0; f < nfinal; ++f) {
-    if (f + 1 == nfinal) {
-      w[14] = total >> 29;  // GetBitCountHi for a 32-bit byte count
-      w[15] = total << 3;   // GetBitCountLo
-    }
+  if (second || r < 56) {
+    w[14] = total >> 29;  // GetBitCountHi for a 32-bit byte count
+    w[15] = total << 3;   // GetBitCountLo
+  }
+}
+
+// Final one or two compressions of a chunk whose full blocks are done (the
+// lane kernel's tail; the pc kernel's producer builds the same words with
+// final_block instead).
+__device__ __forceinline__ void finish(Digest& s, const uint8_t* tail, uint32_t r, uint32_t total) {
+  uint32_t w[16];
+  final_block(w, tail, r, total, false);
+  if (r >= 56) {
     compress(s, w);
 #pragma unroll
-    for (int k = 0; k < 16; ++k) w[k] = 0;  // second final block: zeros + length
+    for (int k = 0; k < 16; ++k) w[k] = 0;
+    w[14] = total >> 29;
+    w[15] = total << 3;
   }
+  compress(s, w);
 }
 
 // splitmix64 counter-mode synthetic stream; identical to

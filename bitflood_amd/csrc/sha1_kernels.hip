@@ -100,6 +100,225 @@ __global__ void __launch_bounds__(256) sha1_lane_kernel(ChunkParams p) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Kernel "pc" (variant 2): producer/consumer split for few chains.
+//
+// With few chunks (C2: 16,384 chains = 256 waves for 1,024 SIMDs) a lone wave
+// issues at most one VALU every ~4 cycles (tools/probe_issue.hip), so the time
+// per chunk is set by the instruction count of ONE chain.  The 64-word message
+// expansion and the byte swaps do not depend on the chain state, so a producer
+// wave on another SIMD computes them and hands the 80 expanded words per block
+// over in LDS; the consumer wave runs only the 80 rounds (5 VALU each).
+//
+// One workgroup = 64 chains = 2 waves: wave 0 consumes, wave 1 produces.  The
+// LDS ring has 2 slots of [20 uint4][64 lanes] (20 KiB each); one workgroup
+// barrier per block step separates "producer writes slot k+1" from "consumer
+// reads slot k".  The producer keeps kPcPrefetch blocks of raw chunk bytes in
+// flight in registers.  Final (padding/length) blocks are built by the
+// producer as ordinary steps, so the consumer loop is uniform.
+// ---------------------------------------------------------------------------
+constexpr int kPcLanes = 64;
+constexpr int kPcQuads = 20;                       // 80 words per block step
+constexpr int kPcSlotU4 = kPcQuads * kPcLanes;     // uint4 per W slot (20 KiB)
+constexpr int kPcRawSlots = 4;                     // raw blocks in flight: steps k..k+3
+constexpr int kPcRawU4 = 4 * kPcLanes;             // uint4 per raw slot (4 KiB)
+// LDS: kRing W slots (20 KiB each) then 4 raw slots (4 KiB each).  kRing = 2
+// is 56 KiB: at most two workgroups share a CU, i.e. four waves on four SIMDs,
+// so a consumer never shares its SIMD with another wave.
+template <int kRing>
+constexpr int pc_lds_bytes() { return (kRing * kPcSlotU4 + kPcRawSlots * kPcRawU4) * 16; }
+
+#ifdef LBF_PC_STAMPS
+// Diagnostic build only (tools/probe_pc.hip): per-workgroup cycle split of the
+// two roles.  [wg][wave][0..3] = {wait-a, work, wait-b, steps}.
+__device__ unsigned long long g_pc_stamps[8192 * 8];
+#define PC_STAMP(var)                                                                 \
+  do {                                                                                \
+    __builtin_amdgcn_sched_barrier(0);                                                \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(var)::"memory");     \
+    __builtin_amdgcn_sched_barrier(0);                                                \
+  } while (0)
+#define PC_ACC(slot, a, b) acc[slot] += (b) - (a)
+#else
+#define PC_STAMP(var) \
+  do {                \
+  } while (0)
+#define PC_ACC(slot, a, b) \
+  do {                     \
+  } while (0)
+#endif
+
+// Valid 64-byte source for lanes with nothing to prefetch (inactive lanes,
+// steps past a chain's full blocks, misaligned chains): the raw-block DMA is
+// issued by every lane every step so that the vmcnt bookkeeping is static.
+__device__ uint4 g_pc_dummy[4];
+
+struct ChainInfo {
+  const uint8_t* src;
+  uint32_t size;
+  uint32_t nfull;   // full 64-byte blocks
+  uint32_t total;   // full + final blocks (0 for an inactive lane)
+  bool aligned;
+};
+
+template <bool kUniform>
+__device__ __forceinline__ ChainInfo chain_info(const ChunkParams& p, uint32_t i) {
+  ChainInfo c{};
+  if (i >= p.n) {
+    c.src = p.base;
+    return c;
+  }
+  uint64_t off;
+  if (kUniform) {
+    off = (p.first_chunk + i) * (uint64_t)p.chunk_size;
+    const uint64_t rem = p.len - off;
+    c.size = rem < p.chunk_size ? (uint32_t)rem : p.chunk_size;
+  } else {
+    off = p.offsets[i];
+    c.size = p.sizes[i];
+  }
+  c.src = p.base + off;
+  c.nfull = c.size >> 6;
+  c.total = c.nfull + ((c.size & 63u) >= 56u ? 2u : 1u);
+  c.aligned = (reinterpret_cast<uintptr_t>(c.src) & 15u) == 0;
+  return c;
+}
+
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, off, 64));
+  return v;
+}
+
+// 16 bytes per lane, global -> LDS (M0 + lane*16), without a VGPR round trip.
+// Inline asm on purpose: with the __builtin_amdgcn_global_load_lds form hipcc
+// drains vmcnt(0) before every later ds_read (it cannot tell the staging slots
+// apart), which would collapse the prefetch; here the waits are counted by hand
+// (pc_wait_raw) and the compiler sees no outstanding VMEM op of ours.
+__device__ __forceinline__ void dma16(const void* g, uint32_t lds_addr) {
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
+               :
+               : "v"(g), "s"(lds_addr)
+               : "memory");
+}
+
+// Raw bytes of block `step` of every chain into raw slot step % 4, laid out
+// [16-byte piece j][lane] so both the DMA and the later ds_read_b128 are
+// contiguous across lanes.  Always exactly 4 VMEM instructions.
+__device__ __forceinline__ void pc_dma_step(const ChainInfo& c, uint32_t step, uint32_t raw_lds) {
+  const bool ok = c.aligned && step < c.nfull;
+  const uint8_t* src = ok ? c.src + 64ull * step : reinterpret_cast<const uint8_t*>(g_pc_dummy);
+  const uint32_t slot = raw_lds + (step % kPcRawSlots) * (kPcRawU4 * 16);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) dma16(src + 16 * j, slot + j * (kPcLanes * 16));
+}
+
+template <int kRing>
+__device__ __forceinline__ void pc_produce(uint4* ring, const ChainInfo& c, uint32_t step, int lane) {
+  uint32_t w[16];
+  if (step < c.nfull) {
+    if (c.aligned) {
+      const uint4* raw = ring + kRing * kPcSlotU4 + (step % kPcRawSlots) * kPcRawU4 + lane;
+      block_from_vec(w, raw[0], raw[kPcLanes], raw[2 * kPcLanes], raw[3 * kPcLanes]);
+    } else {
+      load_words_any(w, c.src + 64ull * step, 64);
+#pragma unroll
+      for (int k = 0; k < 16; ++k) w[k] = bswap(w[k]);
+    }
+  } else {
+    // step == nfull: block with the tail bytes; step == nfull + 1: zeros + length.
+    // Steps past `total` produce don't-care words the consumer never reads.
+    final_block(w, c.src + 64ull * c.nfull, c.size & 63u, c.size, step != c.nfull);
+  }
+  expand_store(w, ring + (step % kRing) * kPcSlotU4 + lane, kPcLanes);
+}
+
+// kRing = 2 (the shipped form): the producer writes step k+1 into slot
+// (k+1) % 2 while the consumer computes step k from slot k % 2.  A 3-slot ring
+// that let the consumer prefetch step k+1 across the barrier measured 6 % slower
+// (extra VGPR traffic and LDS instructions inside the round chain).
+template <bool kUniform, int kRing>
+__global__ void __launch_bounds__(128) sha1_pc_kernel(ChunkParams p) {
+  extern __shared__ __attribute__((aligned(16))) uint4 ring[];  // W[kRing][20][64] | raw[4][4][64]
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const uint32_t i = blockIdx.x * kPcLanes + lane;
+  const ChainInfo c = chain_info<kUniform>(p, i);
+  // Identical in both waves; readfirstlane makes the loop bounds scalar so the
+  // barrier loops are uniform control flow.
+  const uint32_t nsteps = __builtin_amdgcn_readfirstlane(wave_max(c.total));
+  const uint32_t nbarriers = nsteps;  // both waves pass exactly nsteps barriers
+  constexpr uint32_t kAhead = kRing - 1;  // steps the producer runs ahead
+#ifdef LBF_PC_STAMPS
+  unsigned long long acc[4] = {0, 0, 0, 0}, t0 = 0, t1 = 0, t2 = 0, t3 = 0;
+#endif
+
+  if (wave == 1) {
+    // ---------------- producer ----------------
+    const uint32_t raw_lds = (uint32_t)reinterpret_cast<uintptr_t>(ring + kRing * kPcSlotU4);
+#pragma unroll
+    for (uint32_t s = 0; s < kPcRawSlots; ++s) pc_dma_step(c, s, raw_lds);
+    // steps 0 .. kAhead-1 before the first barrier, then step k + kAhead in interval k
+    for (uint32_t k = 0; k < nbarriers + kAhead - 1; ++k) {
+      if (k < nsteps) {
+        PC_STAMP(t0);
+        // raw block k has landed once at most the 3 younger steps (12 DMAs) are pending
+        asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+        PC_STAMP(t1);
+        pc_produce<kRing>(ring, c, k, lane);
+        pc_dma_step(c, k + kPcRawSlots, raw_lds);  // reuses slot k % 4 (read above)
+        PC_STAMP(t2);
+        PC_ACC(0, t0, t1);
+        PC_ACC(1, t1, t2);
+      }
+      PC_STAMP(t2);
+      if (k + 1 >= kAhead) __syncthreads();       // barrier (k + 1 - kAhead)
+      PC_STAMP(t3);
+      PC_ACC(2, t2, t3);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA outlives the workgroup
+  } else {
+    // ---------------- consumer ----------------
+    Digest s;
+    s.init();
+    for (uint32_t k = 0; k < nsteps; ++k) {
+      PC_STAMP(t0);
+      __syncthreads();  // barrier k: slot k % 2 complete
+      PC_STAMP(t1);
+      if (k < c.total) compress_expanded(s, ring + (k % kRing) * kPcSlotU4 + lane, kPcLanes);
+      PC_STAMP(t2);
+      PC_ACC(0, t0, t1);
+      PC_ACC(1, t1, t2);
+    }
+    if (i < p.n) {
+      uint32_t be[5];
+#pragma unroll
+      for (int k = 0; k < 5; ++k) be[k] = bswap(s.h[k]);
+      if (p.digests) {
+        uint32_t* o = reinterpret_cast<uint32_t*>(p.digests + 20ull * i);
+#pragma unroll
+        for (int k = 0; k < 5; ++k) o[k] = be[k];
+      }
+      if (p.verdicts) {
+        const uint32_t* e = reinterpret_cast<const uint32_t*>(p.expected + 20ull * i);
+        uint32_t diff = 0;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) diff |= be[k] ^ e[k];
+        p.verdicts[i] = diff == 0 ? 1 : 0;
+      }
+    }
+  }
+#ifdef LBF_PC_STAMPS
+  if (lane == 0) {
+    unsigned long long* o = g_pc_stamps + (blockIdx.x * 2 + wave) * 4;
+    o[0] = acc[0];
+    o[1] = acc[1];
+    o[2] = acc[2];
+    o[3] = nsteps;
+  }
+#endif
+}
+
 // Counter-mode splitmix64 fill, 16 bytes per thread per step.
 __global__ void __launch_bounds__(256) fill_synth_kernel(uint8_t* dst, uint64_t len, uint64_t seed,
                                                          uint64_t start_word) {
@@ -126,19 +345,35 @@ __global__ void __launch_bounds__(256) fill_synth_kernel(uint8_t* dst, uint64_t 
 }
 
 std::atomic<int> g_variant{0};
+// Chain count up to which the pc kernel is chosen automatically (tuned on
+// MI355X, see DESIGN.md "kernel selection").
+constexpr uint32_t kPcMaxChains = 32768;
 
 }  // namespace
 
 int launch_chunks(const ChunkParams& p, hipStream_t stream) {
   if (p.n == 0) return LBF_OK;
-  // Few chains (C2: 16,384) -> 64-thread workgroups so the waves spread over
-  // every CU; many chains -> 256-thread workgroups.
-  const uint32_t threads = p.n <= 65536u ? 64u : 256u;
-  const uint32_t blocks = (p.n + threads - 1) / threads;
-  if (p.offsets) {
-    hipLaunchKernelGGL(sha1_lane_kernel<false>, dim3(blocks), dim3(threads), 0, stream, p);
+  int variant = g_variant.load();
+  if (variant == 0) {
+    // Few chains: the per-chain instruction count bounds the time, so split the
+    // schedule off to producer waves.  Many chains: every SIMD is busy and the
+    // fused one-chunk-per-lane kernel issues the fewest instructions in total.
+    variant = p.n <= kPcMaxChains ? 2 : 1;
+  }
+  if (variant == 2) {
+    const uint32_t blocks = (p.n + kPcLanes - 1) / kPcLanes;
+    constexpr int lds = pc_lds_bytes<2>();
+    if (p.offsets) hipLaunchKernelGGL((sha1_pc_kernel<false, 2>), dim3(blocks), dim3(128), lds, stream, p);
+    else hipLaunchKernelGGL((sha1_pc_kernel<true, 2>), dim3(blocks), dim3(128), lds, stream, p);
   } else {
-    hipLaunchKernelGGL(sha1_lane_kernel<true>, dim3(blocks), dim3(threads), 0, stream, p);
+    // 64-thread workgroups while waves are scarce so they spread over every CU.
+    const uint32_t threads = p.n <= 65536u ? 64u : 256u;
+    const uint32_t blocks = (p.n + threads - 1) / threads;
+    if (p.offsets) {
+      hipLaunchKernelGGL(sha1_lane_kernel<false>, dim3(blocks), dim3(threads), 0, stream, p);
+    } else {
+      hipLaunchKernelGGL(sha1_lane_kernel<true>, dim3(blocks), dim3(threads), 0, stream, p);
+    }
   }
   LBF_HIP_TRY(hipGetLastError());
   return LBF_OK;
@@ -201,7 +436,7 @@ extern "C" int lbf_sha1_uniform_launch(const uint8_t* d_base, uint64_t len, uint
 }
 
 extern "C" int lbf_set_kernel_variant(int variant) {
-  if (variant < 0 || variant > 1) return fail(LBF_ERR_INVALID, "unknown kernel variant");
+  if (variant < 0 || variant > 2) return fail(LBF_ERR_INVALID, "unknown kernel variant");
   lbf::g_variant.store(variant);
   return LBF_OK;
 }

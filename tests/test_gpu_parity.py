@@ -20,6 +20,16 @@ from bitflood_amd import hashing as H
 pytestmark = pytest.mark.gpu
 SEED_C = 0x5EED
 
+# kernel variants: 1 = one chunk per lane ("lane"), 2 = producer/consumer ("pc")
+VARIANTS = [1, 2]
+
+
+@pytest.fixture(params=VARIANTS, ids=lambda v: {1: "lane", 2: "pc"}[v])
+def variant(request):
+    H.set_kernel_variant(request.param)
+    yield request.param
+    H.set_kernel_variant(0)
+
 
 def _kat_message(k):
     if k["text"] is not None:
@@ -29,27 +39,27 @@ def _kat_message(k):
     return bytes(k["len"])
 
 
-def test_kats(hasher, golden):
+def test_kats(variant, hasher, golden):
     for k in golden("kat.json")["kats"]:
         m = _kat_message(k)
         assert hasher.sha1(m).hex() == k["hex"], k["name"]
         assert hasher.base64_encode(m) == k["b64_27"], k["name"]
 
 
-def test_tails(hasher, oracle, golden):
+def test_tails(variant, hasher, oracle, golden):
     for t in golden("synthetic.json")["tails"]:
         data = oracle.synth(t["seed"], 0, t["size"])
         assert hasher.encode_buffer(data, t["chunk_size"]) == t["b64"], (t["size"], t["chunk_size"])
 
 
-def test_ragged_misaligned(hasher, oracle, golden):
+def test_ragged_misaligned(variant, hasher, oracle, golden):
     r = golden("synthetic.json")["ragged"]
     buf = oracle.synth(r["seed"], 0, r["buf_len"])
     got = hasher.hash_chunks(buf, r["offsets"], r["sizes"])
     assert [bytes(d).hex() for d in got] == r["hex"]
 
 
-def test_random_batch_vs_oracle(hasher, oracle):
+def test_random_batch_vs_oracle(variant, hasher, oracle):
     rng = np.random.default_rng(11)
     buf = oracle.synth(12, 0, 24 << 20)
     n = 3000
@@ -63,7 +73,7 @@ def test_random_batch_vs_oracle(hasher, oracle):
     assert bad.size == 0, f"{bad.size} mismatches, first at {bad[:5]} sizes {sizes[bad[:5]]}"
 
 
-def test_empty_inputs(hasher):
+def test_empty_inputs(variant, hasher):
     assert hasher.sha1(b"").hex() == "da39a3ee5e6b4b0d3255bfef95601890afd80709"
     out = hasher.hash_chunks(np.zeros(16, np.uint8), np.zeros(0, np.uint64), np.zeros(0, np.uint32))
     assert out.shape == (0, 20)
@@ -73,7 +83,7 @@ def test_empty_inputs(hasher):
     assert bytes(d[2]) == hashlib.sha1(bytes([5])).digest()
 
 
-def test_c1(hasher, oracle, golden):
+def test_c1(variant, hasher, oracle, golden):
     c1 = golden("c1.json")
     data = oracle.synth(c1["seed"], 0, c1["size"])
     assert hasher.encode_buffer(data, c1["chunk_size"]) == c1["b64"]
@@ -82,7 +92,7 @@ def test_c1(hasher, oracle, golden):
     assert hasher.encode_buffer(data, o["chunk_size"]) == o["b64"]
 
 
-def test_verify_round_trip(hasher, oracle):
+def test_verify_round_trip(variant, hasher, oracle):
     data = oracle.synth(21, 0, 8 << 20)
     offs, sizes = chunk_table(data.size, 65536)
     exp = hasher.hash_chunks(data, offs, sizes)
@@ -98,7 +108,7 @@ def test_verify_round_trip(hasher, oracle):
     assert np.nonzero(~v)[0].tolist() == [5]
 
 
-def test_small_slots_and_oversize_chunks(oracle):
+def test_small_slots_and_oversize_chunks(variant, oracle):
     """Force many staging groups (1 MiB slots) and the oversize-chunk path."""
     os.environ["LBF_SLOT_MB"] = "1"
     try:
@@ -131,7 +141,7 @@ def test_device_fill_matches_oracle_stream(oracle):
         buf.free()
 
 
-def test_device_ptr_batch(hasher, oracle):
+def test_device_ptr_batch(variant, hasher, oracle):
     from bitflood_amd import _capi
     data = oracle.synth(41, 0, 1 << 20)
     offs = np.array([0, 64, 129, 4096, 70000], dtype=np.uint64)
@@ -151,7 +161,7 @@ def test_device_ptr_batch(hasher, oracle):
             b.free()
 
 
-def test_uniform_partial_last_chunk(oracle):
+def test_uniform_partial_last_chunk(variant, oracle):
     n_bytes = (5 << 20) + 12345
     buf = DeviceBuffer(n_bytes)
     dig = DeviceBuffer(21 * 20)
@@ -172,7 +182,7 @@ def test_uniform_partial_last_chunk(oracle):
         dig.free()
 
 
-def test_c2_full_size_device_resident(golden, oracle):
+def test_c2_full_size_device_resident(variant, golden, oracle):
     """C2: one 4 GiB file, 256 KiB chunks, entirely in HBM."""
     c2 = golden("c2.json")
     size, cs, n = c2["size"], c2["chunk_size"], c2["n_chunks"]

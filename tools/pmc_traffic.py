@@ -1,0 +1,104 @@
+#!/usr/bin/env python3
+"""Summarise a tools/profile_round.sh output directory into profiles/.
+
+HBM traffic per launch of the chunk-hash kernel, corrected as
+/opt/skills/guides/MI355X_MICROARCH.md §HBM prescribes for gfx950:
+  FETCH_SIZE (KiB) reports exactly half the bytes of a wide coalesced stream
+  -> read bytes = 2 * FETCH_SIZE * 1024;  WRITE_SIZE (KiB) is exact for 16-B
+  stores (uncalibrated for the 4-B digest stores, which are < 0.01 % here).
+Also derives the effective clock from GRBM_GUI_ACTIVE (sum over 8 XCDs) and
+the wave-cycle split (active / waiting on memory / issue-stalled).
+
+Usage: tools/pmc_traffic.py gpurun_out/prof/<tag> profiles/<round>/<tag> [--file-bytes N]
+Writes <dst>/summary.json, copies the kernel-stats CSV, and (with
+--record) updates profiles/pmc_traffic.json read by bench.py.
+"""
+import argparse
+import collections
+import csv
+import json
+import os
+import shutil
+
+
+def per_kernel(path):
+    agg = collections.defaultdict(lambda: collections.defaultdict(list))
+    durs = collections.defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        k = r["Kernel_Name"]
+        agg[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        durs[k].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    return agg, durs
+
+
+def mean(x):
+    return sum(x) / len(x) if x else None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("src")
+    ap.add_argument("dst")
+    ap.add_argument("--file-bytes", type=int, default=4 << 30)
+    ap.add_argument("--kernel", default="sha1_")
+    ap.add_argument("--record", action="store_true")
+    a = ap.parse_args()
+    os.makedirs(a.dst, exist_ok=True)
+    out = {"file_bytes": a.file_bytes}
+
+    stats = os.path.join(a.src, "trace", "trace_kernel_stats.csv")
+    if os.path.exists(stats):
+        shutil.copy(stats, os.path.join(a.dst, "kernel_stats.csv"))
+        for r in csv.DictReader(open(stats)):
+            if a.kernel in r["Name"]:
+                out["kernel"] = r["Name"]
+                out["trace_avg_ns"] = float(r["AverageNs"])
+                out["trace_calls"] = int(r["Calls"])
+
+    def pick(sub):
+        p = os.path.join(a.src, sub, "pmc_counter_collection.csv")
+        if not os.path.exists(p):
+            return {}, {}
+        agg, durs = per_kernel(p)
+        for k in agg:
+            if a.kernel in k:
+                return agg[k], durs[k]
+        return {}, {}
+
+    fetch, _ = pick("pmc_fetch")
+    write, _ = pick("pmc_write")
+    sq, sq_durs = pick("pmc_sq")
+    if fetch:
+        rd = 2 * mean(fetch["FETCH_SIZE"]) * 1024
+        out["fetch_size_kib"] = mean(fetch["FETCH_SIZE"])
+        out["read_bytes_per_launch"] = rd
+    if write:
+        out["write_size_kib"] = mean(write["WRITE_SIZE"])
+        out["write_bytes_per_launch"] = mean(write["WRITE_SIZE"]) * 1024
+    if fetch and write:
+        out["hbm_bytes_per_launch"] = out["read_bytes_per_launch"] + out["write_bytes_per_launch"]
+        out["traffic_over_algorithmic"] = out["hbm_bytes_per_launch"] / a.file_bytes
+    if sq:
+        wc = mean(sq["SQ_WAVE_CYCLES"])
+        out["sq"] = {k: mean(v) for k, v in sq.items()}
+        out["wave_cycle_split"] = {
+            "active_inst_any": mean(sq["SQ_ACTIVE_INST_ANY"]) / wc,
+            "wait_any(memory/barrier)": mean(sq["SQ_WAIT_ANY"]) / wc,
+            "wait_inst_any(issue)": mean(sq["SQ_WAIT_INST_ANY"]) / wc,
+        }
+        if sq_durs:
+            out["effective_clock_ghz"] = mean(sq["GRBM_GUI_ACTIVE"]) / 8 / mean(sq_durs)
+    with open(os.path.join(a.dst, "summary.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps(out, indent=1))
+    if a.record and "hbm_bytes_per_launch" in out:
+        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        rec = {"file_bytes": a.file_bytes, "hbm_bytes_per_launch": out["hbm_bytes_per_launch"],
+               "source": os.path.relpath(os.path.join(a.dst, "summary.json"), root),
+               "kernel": out.get("kernel")}
+        with open(os.path.join(root, "profiles", "pmc_traffic.json"), "w") as f:
+            json.dump(rec, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,53 @@
+// tools/probe_pc.hip -- diagnostic build of the pc kernel with s_memtime stamps
+// (not product code).  Compiles the product sources with LBF_PC_STAMPS and
+// prints, per role, the mean cycles per block step spent waiting vs working.
+// Build: hipcc --offload-arch=gfx950 -O3 -DLBF_PC_STAMPS -I../include -I../bitflood_amd/csrc \
+//          probe_pc.hip -o build/probe_pc
+#include "../bitflood_amd/csrc/lbf_capi.cpp"
+#include "../bitflood_amd/csrc/sha1_kernels.hip"
+
+#include <stdio.h>
+#include <vector>
+
+static void run(int variant, uint8_t* buf, uint64_t len, uint32_t cs, uint8_t* dig) {
+  const uint64_t n = len / cs;
+  lbf_set_kernel_variant(variant);
+  float ms = 0;
+  lbf_time_uniform(buf, len, cs, 0, n, dig, 1, nullptr, &ms);
+  if (lbf_time_uniform(buf, len, cs, 0, n, dig, 3, nullptr, &ms)) {
+    printf("error: %s\n", lbf_last_error());
+    return;
+  }
+  const int wgs = (int)((n + 63) / 64);
+  std::vector<unsigned long long> h(wgs * 8);
+  hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(lbf::g_pc_stamps), wgs * 8 * 8, 0, hipMemcpyDeviceToHost);
+  double a[2][3] = {{0}};
+  double steps = 0;
+  for (int w = 0; w < wgs; ++w)
+    for (int r = 0; r < 2; ++r) {
+      for (int j = 0; j < 3; ++j) a[r][j] += (double)h[(w * 2 + r) * 4 + j];
+      if (r == 0) steps += (double)h[(w * 2) * 4 + 3];
+    }
+  steps /= wgs;
+  for (int r = 0; r < 2; ++r)
+    for (int j = 0; j < 3; ++j) a[r][j] /= wgs * steps;
+  printf("variant %d cs=%u n=%lu: %.3f ms (%.1f GiB/s)  steps=%.0f  cycles/step: consumer[wait %.0f work %.0f] "
+         "producer[vmwait %.0f work %.0f barrier %.0f]\n",
+         variant, cs, (unsigned long)n, ms, len / (ms * 1e-3) / (1 << 30), steps, a[0][0], a[0][1], a[1][0],
+         a[1][1], a[1][2]);
+}
+
+int main() {
+  const uint64_t len = 4ull << 30;
+  uint8_t *buf, *dig;
+  hipMalloc(&buf, len);
+  hipMalloc(&dig, (len / 65536) * 20);
+  lbf_fill_synthetic(buf, len, 0x5EED, 0, nullptr);
+  hipDeviceSynchronize();
+  for (int v : {3, 2}) {
+    run(v, buf, len, 262144, dig);
+    run(v, buf, len / 2, 262144, dig);
+    run(v, buf, len, 1 << 20, dig);
+  }
+  return 0;
+}
