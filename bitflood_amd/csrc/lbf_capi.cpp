@@ -11,7 +11,9 @@
 // Multiple devices take contiguous index ranges, one host thread each, with no
 // collective.
 #include <hip/hip_runtime.h>
+#include <fcntl.h>
 #include <string.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <cstdlib>
@@ -173,6 +175,7 @@ struct Slot {
   uint8_t* h_dig = nullptr;
   uint8_t* h_exp = nullptr;
   uint8_t* h_ver = nullptr;
+  uint8_t* h_ok = nullptr;         // 1 = chunk bytes fully available
   // pending group to finalize after the stream drains
   bool pending = false;
   uint64_t g_begin = 0, g_end = 0;
@@ -219,6 +222,7 @@ int worker_init(Worker& w, int device) {
     LBF_HIP_TRY(hipHostMalloc((void**)&s.h_dig, w.desc_cap * 20, hipHostMallocDefault));
     LBF_HIP_TRY(hipHostMalloc((void**)&s.h_exp, w.desc_cap * 20, hipHostMallocDefault));
     LBF_HIP_TRY(hipHostMalloc((void**)&s.h_ver, w.desc_cap, hipHostMallocDefault));
+    s.h_ok = new uint8_t[w.desc_cap];
   }
   return LBF_OK;
 }
@@ -231,14 +235,35 @@ void worker_free(Worker& w) {
     hipFree(s.d_dig); hipFree(s.d_exp); hipFree(s.d_ver);
     hipHostFree(s.h_data); hipHostFree(s.h_off); hipHostFree(s.h_size);
     hipHostFree(s.h_dig); hipHostFree(s.h_exp); hipHostFree(s.h_ver);
+    delete[] s.h_ok;
     if (s.stream) hipStreamDestroy(s.stream);
     s = Slot{};
   }
 }
 
+// Where a job's bytes come from: caller memory (bounds-checked up front) or a
+// file read with pread.  read() returns the bytes actually available.
+struct Source {
+  const uint8_t* base = nullptr;  // memory source
+  uint64_t base_len = 0;
+  int fd = -1;                    // file source
+  uint64_t read(uint8_t* dst, uint64_t off, uint64_t len) const {
+    if (fd < 0) {
+      memcpy(dst, base + off, len);
+      return len;
+    }
+    uint64_t got = 0;
+    while (got < len) {
+      const ssize_t r = pread(fd, dst + got, len - got, (off_t)(off + got));
+      if (r <= 0) break;  // EOF or error: the rest is unavailable
+      got += (uint64_t)r;
+    }
+    return got;
+  }
+};
+
 struct Job {
-  const uint8_t* base;
-  uint64_t base_len;
+  Source src;
   const uint64_t* offsets;
   const uint32_t* sizes;
   const uint8_t* expected;  // null => hash mode
@@ -246,41 +271,51 @@ struct Job {
   uint8_t* verdicts;        // verify mode output
 };
 
-// Copy finished results of a slot's group to the caller's arrays.
-void finalize(const Job& job, Slot& s) {
-  if (!s.pending) return;
-  const uint64_t cnt = s.g_end - s.g_begin;
-  if (job.expected) memcpy(job.verdicts + s.g_begin, s.h_ver, cnt);
-  else memcpy(job.digests + 20 * s.g_begin, s.h_dig, cnt * 20);
+// Copy finished results of a slot's group to the caller's arrays.  Chunks that
+// were not fully readable: verdict 0 (verify) or an LBF_ERR_IO (hash).
+int finalize(const Job& job, Slot& s) {
+  if (!s.pending) return LBF_OK;
   s.pending = false;
+  const uint64_t cnt = s.g_end - s.g_begin;
+  if (job.expected) {
+    for (uint64_t k = 0; k < cnt; ++k) job.verdicts[s.g_begin + k] = s.h_ver[k] & s.h_ok[k];
+    return LBF_OK;
+  }
+  for (uint64_t k = 0; k < cnt; ++k)
+    if (!s.h_ok[k]) return fail(LBF_ERR_IO, "chunk " + std::to_string(s.g_begin + k) + " could not be read in full");
+  memcpy(job.digests + 20 * s.g_begin, s.h_dig, cnt * 20);
+  return LBF_OK;
 }
 
-// Hash one chunk that does not fit a slot: dedicated device buffer.
+// One chunk that does not fit a slot: a dedicated device buffer.
 int run_oversize(Worker& w, const Job& job, uint64_t i) {
   Slot& s = w.slot[0];
   LBF_HIP_TRY(hipStreamSynchronize(s.stream));
   const uint32_t sz = job.sizes[i];
+  std::vector<uint8_t> host(sz ? sz : 1);
+  const bool ok = job.src.read(host.data(), job.offsets[i], sz) == sz;
+  if (!ok) {
+    if (job.expected) {
+      job.verdicts[i] = 0;
+      return LBF_OK;
+    }
+    return fail(LBF_ERR_IO, "chunk " + std::to_string(i) + " could not be read in full");
+  }
   uint8_t* d = nullptr;
   LBF_HIP_TRY(hipMalloc((void**)&d, sz ? sz : 1));
   int rc = LBF_OK;
   do {
-    if (hipMemcpy(d, job.base + job.offsets[i], sz, hipMemcpyHostToDevice) != hipSuccess) {
+    s.h_off[0] = 0;
+    s.h_size[0] = sz;
+    if (hipMemcpy(d, host.data(), sz, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(s.d_off, s.h_off, 8, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(s.d_size, s.h_size, 4, hipMemcpyHostToDevice) != hipSuccess) {
       rc = fail(LBF_ERR_HIP, "oversize chunk H2D failed");
       break;
     }
-    s.h_off[0] = 0;
-    s.h_size[0] = sz;
-    if (hipMemcpy(s.d_off, s.h_off, 8, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(s.d_size, s.h_size, 4, hipMemcpyHostToDevice) != hipSuccess) {
-      rc = fail(LBF_ERR_HIP, "oversize descriptor H2D failed");
+    if (job.expected && hipMemcpy(s.d_exp, job.expected + 20 * i, 20, hipMemcpyHostToDevice) != hipSuccess) {
+      rc = fail(LBF_ERR_HIP, "oversize expected H2D failed");
       break;
-    }
-    if (job.expected) {
-      memcpy(s.h_exp, job.expected + 20 * i, 20);
-      if (hipMemcpy(s.d_exp, s.h_exp, 20, hipMemcpyHostToDevice) != hipSuccess) {
-        rc = fail(LBF_ERR_HIP, "oversize expected H2D failed");
-        break;
-      }
     }
     rc = lbf_sha1_launch(d, s.d_off, s.d_size, 1, job.expected ? nullptr : s.d_dig,
                          job.expected ? s.d_exp : nullptr, job.expected ? s.d_ver : nullptr, s.stream);
@@ -289,34 +324,33 @@ int run_oversize(Worker& w, const Job& job, uint64_t i) {
       rc = fail(LBF_ERR_HIP, "oversize kernel failed");
       break;
     }
-    if (job.expected) {
-      if (hipMemcpy(job.verdicts + i, s.d_ver, 1, hipMemcpyDeviceToHost) != hipSuccess) rc = LBF_ERR_HIP;
-    } else {
-      if (hipMemcpy(job.digests + 20 * i, s.d_dig, 20, hipMemcpyDeviceToHost) != hipSuccess) rc = LBF_ERR_HIP;
-    }
+    const hipError_t e = job.expected ? hipMemcpy(job.verdicts + i, s.d_ver, 1, hipMemcpyDeviceToHost)
+                                      : hipMemcpy(job.digests + 20 * i, s.d_dig, 20, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) rc = fail(LBF_ERR_HIP, "oversize D2H failed");
   } while (0);
-  hipFree(d);
+  (void)hipFree(d);
   return rc;
 }
 
-// Process descriptors [begin, end) on one device.
+// Process descriptors [begin, end) on one device.  Groups of consecutive
+// descriptors whose covering byte range fits a slot are staged into pinned
+// memory (memcpy or pread), then H2D + kernel + D2H run on the slot's stream
+// while the host stages the next group into the other slot.
 int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
   LBF_HIP_TRY(hipSetDevice(w.device));
   int cur = 0;
   uint64_t i = begin;
   int rc = LBF_OK;
   while (i < end && rc == LBF_OK) {
-    // Oversize chunk: its own path (slots drained first).
     if ((uint64_t)job.sizes[i] + 15 > w.slot_bytes) {
       for (Slot& s : w.slot) {
         LBF_HIP_TRY(hipStreamSynchronize(s.stream));
-        finalize(job, s);
+        if ((rc = finalize(job, s))) break;
       }
-      rc = run_oversize(w, job, i);
+      if (rc == LBF_OK) rc = run_oversize(w, job, i);
       ++i;
       continue;
     }
-    // Group: consecutive descriptors whose covering range fits one slot.
     uint64_t lo = job.offsets[i], hi = lo + job.sizes[i];
     uint64_t j = i + 1;
     while (j < end && j - i < w.desc_cap) {
@@ -329,21 +363,36 @@ int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
     }
     Slot& s = w.slot[cur];
     LBF_HIP_TRY(hipStreamSynchronize(s.stream));
-    finalize(job, s);
+    if ((rc = finalize(job, s))) break;
     const uint64_t cnt = j - i;
-    // Stage bytes and rebased descriptors in pinned memory.  The covered range
-    // [lo, hi) lands at h_data + (lo % 16) so each chunk keeps its offset's
-    // 16-byte phase (aligned chunks take the vector-load path on the device).
+    // The covered range [lo, hi) lands at h_data + (lo % 16) so each chunk
+    // keeps its offset's 16-byte phase (aligned chunks take the vector-load
+    // path on the device).
     const uint64_t shift = lo & 15u;
-    memcpy(s.h_data + shift, job.base + lo, hi - lo);
+    const uint64_t avail = job.src.read(s.h_data + shift, lo, hi - lo);
     for (uint64_t k = 0; k < cnt; ++k) {
-      s.h_off[k] = job.offsets[i + k] - lo + shift;
+      const uint64_t o = job.offsets[i + k];
+      s.h_off[k] = o - lo + shift;
       s.h_size[k] = job.sizes[i + k];
+      s.h_ok[k] = (o + job.sizes[i + k] <= lo + avail) ? 1 : 0;
     }
-    const uint64_t copy_bytes = hi - lo + shift;
+    const uint64_t copy_bytes = avail + shift;
     LBF_HIP_TRY(hipMemcpyAsync(s.d_data, s.h_data, copy_bytes, hipMemcpyHostToDevice, s.stream));
     LBF_HIP_TRY(hipMemcpyAsync(s.d_off, s.h_off, cnt * 8, hipMemcpyHostToDevice, s.stream));
     LBF_HIP_TRY(hipMemcpyAsync(s.d_size, s.h_size, cnt * 4, hipMemcpyHostToDevice, s.stream));
+    // Unreadable chunks must not be hashed from stale slot bytes past `avail`:
+    // give them size 0 on the device (their result is discarded anyway).
+    bool any_short = false;
+    for (uint64_t k = 0; k < cnt; ++k) any_short |= !s.h_ok[k];
+    if (any_short) {
+      for (uint64_t k = 0; k < cnt; ++k)
+        if (!s.h_ok[k]) {
+          s.h_size[k] = 0;
+          s.h_off[k] = 0;
+        }
+      LBF_HIP_TRY(hipMemcpyAsync(s.d_off, s.h_off, cnt * 8, hipMemcpyHostToDevice, s.stream));
+      LBF_HIP_TRY(hipMemcpyAsync(s.d_size, s.h_size, cnt * 4, hipMemcpyHostToDevice, s.stream));
+    }
     if (job.expected) {
       memcpy(s.h_exp, job.expected + 20 * i, cnt * 20);
       LBF_HIP_TRY(hipMemcpyAsync(s.d_exp, s.h_exp, cnt * 20, hipMemcpyHostToDevice, s.stream));
@@ -364,23 +413,22 @@ int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
   for (Slot& s : w.slot) {
     if (hipStreamSynchronize(s.stream) != hipSuccess && rc == LBF_OK)
       rc = fail(LBF_ERR_HIP, "stream synchronize failed");
-    if (rc == LBF_OK) finalize(job, s);
+    if (rc == LBF_OK) rc = finalize(job, s);
     s.pending = false;
   }
   return rc;
 }
 
-int validate_host_job(const Job& job, uint64_t n) {
+int validate_memory_job(const Job& job, uint64_t n) {
   for (uint64_t i = 0; i < n; ++i) {
     const uint64_t o = job.offsets[i], sz = job.sizes[i];
-    if (o > job.base_len || sz > job.base_len - o)
+    if (o > job.src.base_len || sz > job.src.base_len - o)
       return fail(LBF_ERR_INVALID, "chunk " + std::to_string(i) + " lies outside [base, base+base_len)");
   }
   return LBF_OK;
 }
 
 int run_job(lbf_ctx* ctx, const Job& job, uint64_t n) {
-  if (int rc = validate_host_job(job, n)) return rc;
   std::lock_guard<std::mutex> lock(ctx->mu);
   const size_t nw = ctx->workers.size();
   if (nw == 1 || n < 2 * nw) return worker_run(ctx->workers[0], job, 0, n);
@@ -458,7 +506,13 @@ extern "C" int lbf_sha1_batch(lbf_ctx* ctx, const uint8_t* base, uint64_t base_l
   if (!base || !offsets || !sizes || !out_digests) return fail(LBF_ERR_INVALID, "null argument");
   if (flags == LBF_DEVICE_PTR) return run_device_job(ctx, base, offsets, sizes, n, out_digests, nullptr, nullptr);
   if (flags != LBF_HOST_PTR) return fail(LBF_ERR_INVALID, "unknown flags");
-  Job job{base, base_len, offsets, sizes, nullptr, out_digests, nullptr};
+  Job job{};
+  job.src.base = base;
+  job.src.base_len = base_len;
+  job.offsets = offsets;
+  job.sizes = sizes;
+  job.digests = out_digests;
+  if (int rc = validate_memory_job(job, n)) return rc;
   return run_job(ctx, job, n);
 }
 
@@ -470,8 +524,39 @@ extern "C" int lbf_verify_batch(lbf_ctx* ctx, const uint8_t* base, uint64_t base
   if (!base || !offsets || !sizes || !expected || !verdicts) return fail(LBF_ERR_INVALID, "null argument");
   if (flags == LBF_DEVICE_PTR) return run_device_job(ctx, base, offsets, sizes, n, nullptr, expected, verdicts);
   if (flags != LBF_HOST_PTR) return fail(LBF_ERR_INVALID, "unknown flags");
-  Job job{base, base_len, offsets, sizes, expected, nullptr, verdicts};
+  Job job{};
+  job.src.base = base;
+  job.src.base_len = base_len;
+  job.offsets = offsets;
+  job.sizes = sizes;
+  job.expected = expected;
+  job.verdicts = verdicts;
+  if (int rc = validate_memory_job(job, n)) return rc;
   return run_job(ctx, job, n);
+}
+
+extern "C" int lbf_file_ranges(lbf_ctx* ctx, const char* path, const uint64_t* offsets, const uint32_t* sizes,
+                               uint64_t n, const uint8_t* expected, uint8_t* out) {
+  if (!ctx || !path) return fail(LBF_ERR_INVALID, "null context/path");
+  if (n == 0) return LBF_OK;
+  if (!offsets || !sizes || !out) return fail(LBF_ERR_INVALID, "null argument");
+  const int fd = open(path, O_RDONLY | O_CLOEXEC);
+  if (fd < 0) {
+    if (!expected) return fail(LBF_ERR_IO, std::string("cannot open ") + path);
+    memset(out, 0, n);  // Flood.cpp:257: no file -> every chunk stays '0'
+    return LBF_OK;
+  }
+  posix_fadvise(fd, 0, 0, POSIX_FADV_SEQUENTIAL);
+  Job job{};
+  job.src.fd = fd;
+  job.offsets = offsets;
+  job.sizes = sizes;
+  job.expected = expected;
+  if (expected) job.verdicts = out;
+  else job.digests = out;
+  const int rc = run_job(ctx, job, n);
+  close(fd);
+  return rc;
 }
 
 extern "C" int lbf_sha1_one(lbf_ctx* ctx, const uint8_t* data, uint32_t size, uint8_t out[20]) {

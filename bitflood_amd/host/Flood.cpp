@@ -1,0 +1,173 @@
+// Flood.cpp -- the verify paths of the reference's Flood / ChunkMethodHandler,
+// batched onto the GPU (see include/libBitFlood/Flood.H for the mapping).
+#include "libBitFlood/Flood.H"
+
+#include <fcntl.h>
+#include <unistd.h>
+
+#include <cstdio>
+
+#include "lbf_hash.h"
+#include "libBitFlood/Encoder.H"
+
+namespace libBitFlood {
+
+namespace {
+
+// 27-char string -> 20 raw bytes.  A string that is not canonical base64-27
+// can never equal a computed hash, so it yields ok = false (verdict 0 without
+// hashing), exactly what the reference's string compare gives.
+bool decode_hash(const std::string& s, U8* out) {
+  return lbf_b64_27_decode(s.data(), s.size(), out) == LBF_OK;
+}
+
+}  // namespace
+
+std::string Flood::PathOf(const std::string& i_name) const {
+  if (m_rootdir.empty() || (!i_name.empty() && i_name[0] == '/')) return i_name;
+  return m_rootdir + "/" + i_name;
+}
+
+Error::ErrorCode Flood::Initialize(FloodFileSPtr& i_floodfile) {
+  m_floodfile = i_floodfile;
+  return SetupFilesAndChunks();  // Flood.cpp:25-35
+}
+
+// Flood.cpp:220-299.  Per file: lay the chunks out back to back in index
+// order, then hash every chunk that exists on disk in ONE batched verify (the
+// reference does fseek + malloc + fread + Base64Encode + strcmp per chunk).
+Error::ErrorCode Flood::SetupFilesAndChunks() {
+  m_totalbytes = 0;
+  m_runtimefiles.clear();
+  m_chunkstodownload.clear();
+  if (!m_floodfile) return Error::UNKNOWN_ERROR_LBF;
+  lbf_ctx* ctx = Encoder::Context();
+  if (!ctx) return Error::UNKNOWN_ERROR_LBF;
+  Error::ErrorCode ret = Error::NO_ERROR_LBF;
+  for (const auto& kv : m_floodfile->m_files) {
+    const FloodFile::FileSPtr& file = kv.second;
+    m_totalbytes += file->m_size;
+    RuntimeFile rtf;
+    const U64 n = file->m_chunks.size();
+    rtf.m_chunkoffsets.assign(n, 0);
+    rtf.m_chunkmap.assign(n, '0');
+    rtf.m_file = file;
+    // offsets follow chunk vector order (sorted by index in FromXML)
+    V_U64 offs(n);
+    V_U32 sizes(n);
+    V_U8 expected(n * 20, 0);
+    std::vector<U8> decodable(n, 0);
+    U64 next = 0;
+    bool indices_ok = true;
+    std::vector<bool> seen(n, false);
+    for (U64 k = 0; k < n; ++k) {
+      const FloodFile::Chunk& c = file->m_chunks[k];
+      if (c.m_index >= n || seen[c.m_index]) {  // each index 0..n-1 exactly once
+        indices_ok = false;
+        break;
+      }
+      seen[c.m_index] = true;
+      rtf.m_chunkoffsets[c.m_index] = next;
+      offs[k] = next;
+      sizes[k] = c.m_size;
+      decodable[k] = decode_hash(c.m_hash, &expected[20 * k]) ? 1 : 0;
+      next += c.m_size;
+    }
+    if (!indices_ok) {  // the reference asserts (Flood.cpp:253-254)
+      ret = Error::UNKNOWN_ERROR_LBF;
+      continue;
+    }
+    V_U8 verdicts(n, 0);
+    if (n && lbf_file_ranges(ctx, PathOf(file->m_name).c_str(), offs.data(), sizes.data(), n, expected.data(),
+                             verdicts.data()) != LBF_OK) {
+      ret = Error::UNKNOWN_ERROR_LBF;
+      continue;
+    }
+    for (U64 k = 0; k < n; ++k) {
+      const U32 idx = file->m_chunks[k].m_index;
+      if (verdicts[k] && decodable[k]) rtf.m_chunkmap[idx] = '1';
+      if (rtf.m_chunkmap[idx] == '0') m_chunkstodownload.insert(P_ChunkKey(file->m_name, idx));
+    }
+    m_runtimefiles[file->m_name] = rtf;
+  }
+  return ret;
+}
+
+// ChunkMethods.cpp:89-135 (seeder): read the chunk at its offset and send it
+// only if it still hashes to the flood-file value.
+Error::ErrorCode Flood::ReadVerifiedChunk(const std::string& i_filename, U32 i_chunkindex, V_U8& o_data,
+                                          bool& o_valid) {
+  o_valid = false;
+  o_data.clear();
+  auto it = m_runtimefiles.find(i_filename);
+  if (it == m_runtimefiles.end() || i_chunkindex >= it->second.m_file->m_chunks.size())
+    return Error::NO_ERROR_LBF;  // unknown file/chunk: nothing sent
+  const FloodFile::Chunk& chunk = it->second.m_file->m_chunks[i_chunkindex];
+  const U64 off = it->second.m_chunkoffsets[i_chunkindex];
+  const int fd = open(PathOf(i_filename).c_str(), O_RDONLY | O_CLOEXEC);
+  if (fd < 0) return Error::NO_ERROR_LBF;
+  o_data.resize(chunk.m_size);
+  U64 got = 0;
+  while (got < chunk.m_size) {
+    const ssize_t r = pread(fd, o_data.data() + got, chunk.m_size - got, (off_t)(off + got));
+    if (r <= 0) break;
+    got += (U64)r;
+  }
+  close(fd);
+  U8 expected[20];
+  if (got != chunk.m_size || !decode_hash(chunk.m_hash, expected)) {
+    o_data.clear();
+    return Error::NO_ERROR_LBF;
+  }
+  lbf_ctx* ctx = Encoder::Context();
+  if (!ctx) return Error::UNKNOWN_ERROR_LBF;
+  const U64 zero = 0;
+  const U32 sz = chunk.m_size;
+  U8 verdict = 0;
+  static const U8 kEmpty = 0;
+  if (lbf_verify_batch(ctx, sz ? o_data.data() : &kEmpty, sz, &zero, &sz, 1, expected, &verdict, LBF_HOST_PTR) !=
+      LBF_OK)
+    return Error::UNKNOWN_ERROR_LBF;
+  o_valid = verdict != 0;
+  if (!o_valid) o_data.clear();
+  return Error::NO_ERROR_LBF;
+}
+
+// ChunkMethods.cpp:137-225 (receiver): size check, verify on the GPU, write
+// at the chunk's offset, mark it '1' and stop wanting it.  (Broadcasting
+// NotifyHaveChunk and the in-flight bookkeeping belong to the peer loop.)
+Error::ErrorCode Flood::ReceiveChunk(const std::string& i_filename, U32 i_chunkindex, const U8* i_data, U32 i_size,
+                                     bool& o_accepted) {
+  o_accepted = false;
+  auto it = m_runtimefiles.find(i_filename);
+  if (it == m_runtimefiles.end() || i_chunkindex >= it->second.m_file->m_chunks.size())
+    return Error::NO_ERROR_LBF;
+  RuntimeFile& rtf = it->second;
+  const FloodFile::Chunk& chunk = rtf.m_file->m_chunks[i_chunkindex];
+  if (chunk.m_size != i_size) return Error::NO_ERROR_LBF;  // :156
+  U8 expected[20];
+  if (!decode_hash(chunk.m_hash, expected)) return Error::NO_ERROR_LBF;
+  lbf_ctx* ctx = Encoder::Context();
+  if (!ctx) return Error::UNKNOWN_ERROR_LBF;
+  const U64 zero = 0;
+  U8 verdict = 0;
+  static const U8 kEmpty = 0;
+  if (lbf_verify_batch(ctx, i_size ? i_data : &kEmpty, i_size, &zero, &i_size, 1, expected, &verdict,
+                       LBF_HOST_PTR) != LBF_OK)
+    return Error::UNKNOWN_ERROR_LBF;
+  if (!verdict) return Error::NO_ERROR_LBF;  // bad chunk silently dropped (:167)
+  const std::string path = PathOf(i_filename);
+  FILE* f = fopen(path.c_str(), "r+b");  // :169-173
+  if (!f) f = fopen(path.c_str(), "w+b");
+  if (!f) return Error::NO_ERROR_LBF;
+  bool ok = fseeko(f, (off_t)rtf.m_chunkoffsets[i_chunkindex], SEEK_SET) == 0;
+  if (ok) ok = fwrite(i_data, 1, i_size, f) == i_size;
+  fclose(f);
+  if (!ok) return Error::NO_ERROR_LBF;
+  rtf.m_chunkmap[i_chunkindex] = '1';  // :181-185
+  m_chunkstodownload.erase(P_ChunkKey(it->first, i_chunkindex));
+  o_accepted = true;
+  return Error::NO_ERROR_LBF;
+}
+
+}  // namespace libBitFlood

@@ -1,0 +1,135 @@
+// gpu_tests.cpp -- C++ API tests that need the GPU (run by
+// tests/test_host_cpp.py under -m gpu): Base64Encode KATs through the
+// reference signature, the batch extension, and the seeder/receiver verify
+// paths of Flood (ChunkMethods.cpp:89-225 restated) on a real file.
+//   lbf_gpu_tests <scratch-dir>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "libBitFlood/Encoder.H"
+#include "libBitFlood/Flood.H"
+
+using namespace libBitFlood;
+
+static int g_fail = 0;
+#define CHECK(cond)                                                                  \
+  do {                                                                               \
+    if (!(cond)) {                                                                   \
+      std::fprintf(stderr, "%s:%d CHECK failed: %s\n", __FILE__, __LINE__, #cond);   \
+      ++g_fail;                                                                      \
+    }                                                                                \
+  } while (0)
+
+static std::vector<U8> pattern(size_t n, U32 seed) {
+  std::vector<U8> v(n);
+  U32 x = seed * 2654435761u + 1;
+  for (size_t i = 0; i < n; ++i) {
+    x ^= x << 13;
+    x ^= x >> 17;
+    x ^= x << 5;
+    v[i] = (U8)(x >> 24);
+  }
+  return v;
+}
+
+int main(int argc, char** argv) {
+  if (argc < 2) {
+    std::fprintf(stderr, "usage: lbf_gpu_tests <scratch-dir>\n");
+    return 2;
+  }
+  const std::string dir = argv[1];
+  FloodFile::SetResolveTrackerHosts(false);
+
+  // Base64Encode through the reference signature (sha.txt KATs, Encoder.cpp:107-120)
+  std::string s;
+  if (Encoder::Base64Encode((const U8*)"abc", 3, s) != Error::NO_ERROR_LBF) {
+    std::fprintf(stderr, "no GPU path: %s\n", Encoder::LastError());
+    return 1;
+  }
+  CHECK(s == "qZk+NkcGgWq6PiVxeFDCbJzQ2J0");
+  CHECK(Encoder::Base64Encode((const U8*)"", 0, s) == Error::NO_ERROR_LBF);
+  CHECK(s == "2jmj7l5rSw0yVb/vlWAYkK/YBwk");
+  const char* nist = "abcdbcdecdefdefgefghfghighijhijkijkljklmklmnlmnomnopnopq";
+  Encoder::Base64Encode((const U8*)nist, (U32)strlen(nist), s);
+  CHECK(s == "hJg+RBw70m66rkqh+VEp5eVGcPE");
+
+  // batch == per-buffer
+  std::vector<U8> buf = pattern(1 << 20, 3);
+  std::vector<U64> offs = {0, 1, 64, 4096, 100000};
+  std::vector<U32> sizes = {0, 55, 56, 65536, 300000};
+  V_String hs;
+  CHECK(Encoder::Base64EncodeBatch(buf.data(), buf.size(), offs.data(), sizes.data(), offs.size(), hs) ==
+        Error::NO_ERROR_LBF);
+  for (size_t i = 0; i < offs.size() && i < hs.size(); ++i) {
+    std::string one;
+    Encoder::Base64Encode(buf.data() + offs[i], sizes[i], one);
+    CHECK(hs[i] == one);
+  }
+
+  // EncodeFile -> Flood: seeder read-verify, receiver accept/reject
+  const std::string src = dir + "/seed.bin";
+  std::vector<U8> data = pattern(3 * 65536 + 777, 9);
+  FILE* f = std::fopen(src.c_str(), "wb");
+  std::fwrite(data.data(), 1, data.size(), f);
+  std::fclose(f);
+  Encoder::ToEncode e;
+  e.m_files.push_back(src);
+  e.m_chunksize = 65536;
+  e.m_trackers.push_back({"127.0.0.1", 10101});
+  FloodFileSPtr ff(new FloodFile());
+  CHECK(Encoder::EncodeFile(e, *ff) == Error::NO_ERROR_LBF);
+  CHECK(ff->m_files.size() == 1 && ff->m_files[src]->m_chunks.size() == 4);
+  CHECK(ff->m_files[src]->m_size == data.size());
+
+  Flood seeder;
+  CHECK(seeder.Initialize(ff) == Error::NO_ERROR_LBF);
+  CHECK(seeder.m_runtimefiles[src].m_chunkmap == "1111");
+  CHECK(seeder.m_chunkstodownload.empty());
+  V_U8 chunk;
+  bool valid = false;
+  CHECK(seeder.ReadVerifiedChunk(src, 3, chunk, valid) == Error::NO_ERROR_LBF);
+  CHECK(valid && chunk.size() == 777 && std::memcmp(chunk.data(), data.data() + 3 * 65536, 777) == 0);
+
+  // a leecher whose copy lives elsewhere: same flood, empty directory
+  const std::string ldir = dir + "/leech";
+  std::string mk = "mkdir -p '" + ldir + "'";
+  CHECK(std::system(mk.c_str()) == 0);
+  FloodFileSPtr lf(new FloodFile());
+  FloodFile::FileSPtr lfile(new FloodFile::File(*ff->m_files[src]));
+  lfile->m_name = "copy.bin";
+  lf->m_files["copy.bin"] = lfile;
+  Flood leech;
+  leech.m_rootdir = ldir;
+  CHECK(leech.Initialize(lf) == Error::NO_ERROR_LBF);
+  CHECK(leech.m_runtimefiles["copy.bin"].m_chunkmap == "0000");
+  CHECK(leech.m_chunkstodownload.size() == 4);
+  bool accepted = true;
+  std::vector<U8> bad(data.begin() + 65536, data.begin() + 2 * 65536);
+  bad[17] ^= 1;
+  CHECK(leech.ReceiveChunk("copy.bin", 1, bad.data(), (U32)bad.size(), accepted) == Error::NO_ERROR_LBF);
+  CHECK(!accepted);  // corrupted: dropped (ChunkMethods.cpp:167)
+  CHECK(leech.ReceiveChunk("copy.bin", 1, data.data() + 65536, 1000, accepted) == Error::NO_ERROR_LBF);
+  CHECK(!accepted);  // wrong size (ChunkMethods.cpp:156)
+  for (U32 i : {3u, 1u, 0u, 2u}) {  // out of order, like a swarm
+    const U32 sz = i == 3 ? 777 : 65536;
+    CHECK(leech.ReceiveChunk("copy.bin", i, data.data() + 65536ull * i, sz, accepted) == Error::NO_ERROR_LBF);
+    CHECK(accepted);
+  }
+  CHECK(leech.m_runtimefiles["copy.bin"].m_chunkmap == "1111");
+  CHECK(leech.m_chunkstodownload.empty());
+  // the written file re-verifies from scratch (resume after restart)
+  Flood again;
+  again.m_rootdir = ldir;
+  CHECK(again.Initialize(lf) == Error::NO_ERROR_LBF);
+  CHECK(again.m_runtimefiles["copy.bin"].m_chunkmap == "1111");
+
+  if (g_fail) {
+    std::fprintf(stderr, "%d check(s) failed (last error: %s)\n", g_fail, Encoder::LastError());
+    return 1;
+  }
+  std::printf("gpu_tests OK\n");
+  return 0;
+}

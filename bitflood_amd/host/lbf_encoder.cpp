@@ -1,0 +1,62 @@
+// lbf_encoder -- Linux port of /root/reference/cpp/test_encoder/src/test_encoder.cpp
+// (:16-75): encode one file into a flood file.
+//   lbf_encoder <file> http://host:port/ <out.flood> [--chunksize N] [--crlf] [--devices MASK]
+// Same three positional arguments and the same tracker-URL parsing (:44-52);
+// the chunk size the reference hard-wires to 262144 (:56) becomes a flag
+// (config C1 needs 64 KiB).  --crlf writes the CRLF line ends test_encoder's
+// fopen(..., "w") produces on Win32.
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <iostream>
+#include <sstream>
+#include <string>
+
+#include "libBitFlood/Encoder.H"
+#include "libBitFlood/FloodFile.H"
+
+using namespace libBitFlood;
+
+int main(int argc, char* argv[]) {
+  std::vector<std::string> pos;
+  U32 chunksize = 262144;
+  bool crlf = false;
+  for (int i = 1; i < argc; ++i) {
+    const std::string a = argv[i];
+    if (a == "--chunksize" && i + 1 < argc) chunksize = (U32)strtoul(argv[++i], nullptr, 10);
+    else if (a == "--crlf") crlf = true;
+    else if (a == "--devices" && i + 1 < argc) Encoder::SetDeviceMask((U32)strtoul(argv[++i], nullptr, 0));
+    else pos.push_back(a);
+  }
+  if (pos.size() != 3) {
+    std::cerr << "Please use three arguments: the name of the file to encode, the name of the tracker, and the "
+                 "name of the flood file"
+              << std::endl;
+    return 1;
+  }
+  Encoder::ToEncode::Tracker tracker;
+  const std::string url = pos[1];
+  const size_t h_start = url.find("http://") + strlen("http://");
+  const size_t p_start = url.find(':', h_start) + 1;
+  const size_t u_start = url.find('/', p_start) + 1;
+  tracker.first = url.substr(h_start, p_start - h_start - 1);
+  std::stringstream port;
+  port << url.substr(p_start, u_start - p_start - 1);
+  port >> tracker.second;
+
+  Encoder::ToEncode e;
+  e.m_files.push_back(pos[0]);
+  e.m_chunksize = chunksize;
+  e.m_trackers.push_back(tracker);
+
+  FloodFile out;
+  if (Encoder::EncodeFile(e, out) != Error::NO_ERROR_LBF) {
+    std::cerr << "EncodeFile failed: " << Encoder::LastError() << std::endl;
+    return 2;
+  }
+  if (out.ToXMLFile(pos[2], crlf) != Error::NO_ERROR_LBF) {
+    std::cerr << "cannot write " << pos[2] << std::endl;
+    return 3;
+  }
+  return 0;
+}

@@ -83,6 +83,20 @@ int lbf_verify_batch(lbf_ctx* ctx, const uint8_t* base, uint64_t base_len,
                      const uint64_t* offsets, const uint32_t* sizes, uint64_t n,
                      const uint8_t* expected, uint8_t* verdicts, int flags);
 
+/* ---- chunks read straight from a file ------------------------------------
+ * Chunk i = bytes [offsets[i], offsets[i] + sizes[i]) of the file at `path`,
+ * read with pread into the context's pinned staging (no intermediate copy),
+ * overlapped with H2D copies and kernels.  This is EncodeFile's fread loop
+ * (Encoder.cpp:54-72) and _SetupFilesAndChunks' fseek/fread loop
+ * (Flood.cpp:259-275) batched.
+ * expected == NULL: hash mode, `out` receives n*20 digest bytes; a chunk that
+ *   cannot be read in full fails the call with LBF_ERR_IO.
+ * expected != NULL: verify mode, `out` receives n verdict bytes; a chunk that
+ *   cannot be read in full (missing file, past EOF) gets verdict 0, as the
+ *   reference leaves such chunks '0'. */
+int lbf_file_ranges(lbf_ctx* ctx, const char* path, const uint64_t* offsets, const uint32_t* sizes,
+                    uint64_t n, const uint8_t* expected, uint8_t* out);
+
 /* ---- single buffer (Encoder::Base64Encode's hash, host memory) ---------- */
 int lbf_sha1_one(lbf_ctx* ctx, const uint8_t* data, uint32_t size, uint8_t out_digest[20]);
 

@@ -1,0 +1,168 @@
+"""The C++ libBitFlood layer: flood-file format (CPU), the test_encoder port and
+the resume-verify CLI (GPU), and the C++ API tests in lbf_gpu_tests (GPU).
+
+Expected flood-file bytes are built here from the golden chunk strings with the
+Xerces 2.6 DOMWriter pretty-print rules (see bitflood_amd/host/FloodFile.cpp
+for the DOMWriterImpl.cpp citations).  No reference run pins those bytes: the
+format is pinned by code reading.
+"""
+import base64
+import hashlib
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from bitflood_amd import _capi
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "bitflood_amd", "lib")
+ENCODER = os.path.join(LIB, "lbf_encoder")
+VERIFY = os.path.join(LIB, "lbf_verify")
+
+
+def _escape(v: str) -> str:
+    return v.replace("&", "&amp;").replace("<", "&lt;").replace('"', "&quot;").replace("\n", "&#xA;")
+
+
+def expected_xml(files, trackers) -> str:
+    """files: list of (name, size, [(hash, index, size, weight)]) in map order."""
+    x = "\n<BitFlood>\n\n  <FileInfo"
+    if not files:
+        x += "/>"
+    else:
+        x += ">"
+        for name, size, chunks in sorted(files, key=lambda f: f[0].encode()):
+            x += f'\n    <File name="{_escape(name)}" size="{size}"'
+            if not chunks:
+                x += "/>"
+                continue
+            x += ">"
+            for h, i, s, w in chunks:
+                x += f'\n      <Chunk hash="{_escape(h)}" index="{i}" size="{s}" weight="{w}"/>'
+            x += "\n    </File>"
+        x += "\n  </FileInfo>"
+    for host, port in trackers:
+        x += f'\n\n  <Tracker host="{_escape(host)}" port="{port}"/>'
+    return x + "\n\n</BitFlood>"
+
+
+def b64_27(d: bytes) -> str:
+    return base64.b64encode(d).decode().rstrip("=")
+
+
+def test_flood_file_format_unit():
+    out = subprocess.run([os.path.join(LIB, "lbf_host_tests")], capture_output=True, text=True)
+    assert out.returncode == 0, out.stderr
+    assert "host_tests OK" in out.stdout
+
+
+def test_expected_xml_helper_matches_cpp_unit_case():
+    # the same model as host_tests.cpp kExpected, built by the Python restatement
+    x = expected_xml([("a.bin", 70000, [("LgAPp+hXWcf0wlTU2cM+9IHkWac", 0, 65536, 0),
+                                         ("qZk+NkcGgWq6PiVxeFDCbJzQ2J0", 1, 4464, 0)]),
+                      ('b&c"<d>\n.bin', 0, [])], [("127.0.0.1", 10101)])
+    assert x.startswith('\n<BitFlood>\n\n  <FileInfo>\n    <File name="a.bin" size="70000">')
+    assert '<File name="b&amp;c&quot;&lt;d>&#xA;.bin" size="0"/>' in x
+    assert x.endswith('\n\n  <Tracker host="127.0.0.1" port="10101"/>\n\n</BitFlood>')
+
+
+@pytest.mark.skipif(_capi.device_count() > 0, reason="only meaningful without a GPU")
+def test_encoder_cli_fails_loudly_without_gpu(tmp_path):
+    f = tmp_path / "x.bin"
+    f.write_bytes(b"abc")
+    out = subprocess.run([ENCODER, str(f), "http://127.0.0.1:10101/", str(tmp_path / "x.flood")],
+                         capture_output=True, text=True)
+    assert out.returncode == 2
+    assert "no CPU fallback" in out.stderr
+
+
+def test_encoder_cli_usage():
+    out = subprocess.run([ENCODER, "only-one-arg"], capture_output=True, text=True)
+    assert out.returncode == 1
+    assert "three arguments" in out.stderr
+
+
+# ----------------------------------------------------------------------------- GPU
+@pytest.mark.gpu
+@pytest.mark.parametrize("crlf", [False, True])
+def test_encoder_cli_c1(tmp_path, oracle, golden, crlf):
+    """C1: one 16 MiB file at 64 KiB chunks -> flood file, byte-exact."""
+    c1 = golden("c1.json")
+    (tmp_path / "c1.bin").write_bytes(oracle.synth(c1["seed"], 0, c1["size"]).tobytes())
+    args = [ENCODER, "c1.bin", "http://127.0.0.1:10101/", "c1.flood", "--chunksize", str(c1["chunk_size"])]
+    if crlf:
+        args.append("--crlf")
+    out = subprocess.run(args, cwd=tmp_path, capture_output=True, text=True)
+    assert out.returncode == 0, out.stderr
+    chunks = [(h, i, c1["chunk_size"], 0) for i, h in enumerate(c1["b64"])]
+    want = expected_xml([("c1.bin", c1["size"], chunks)], [("127.0.0.1", 10101)])
+    if crlf:
+        want = want.replace("\n", "\r\n")
+    assert (tmp_path / "c1.flood").read_bytes() == want.encode()
+
+
+@pytest.mark.gpu
+def test_encoder_cli_default_chunksize_odd_tail(tmp_path, oracle, golden):
+    o = golden("c1.json")["odd_tail"]
+    (tmp_path / "odd.bin").write_bytes(oracle.synth(o["seed"], 0, o["size"]).tobytes())
+    out = subprocess.run([ENCODER, "odd.bin", "http://localhost:4000/", "odd.flood"], cwd=tmp_path,
+                         capture_output=True, text=True)
+    assert out.returncode == 0, out.stderr
+    n = len(o["b64"])
+    sizes = [262144] * (n - 1) + [o["size"] - 262144 * (n - 1)]
+    chunks = [(h, i, sizes[i], 0) for i, h in enumerate(o["b64"])]
+    assert (tmp_path / "odd.flood").read_text() == expected_xml([("odd.bin", o["size"], chunks)],
+                                                                [("localhost", 4000)])
+
+
+@pytest.mark.gpu
+def test_encoder_cli_empty_file(tmp_path):
+    (tmp_path / "empty.bin").write_bytes(b"")
+    out = subprocess.run([ENCODER, "empty.bin", "http://127.0.0.1:1/", "e.flood"], cwd=tmp_path,
+                         capture_output=True, text=True)
+    assert out.returncode == 0, out.stderr
+    assert (tmp_path / "e.flood").read_text() == expected_xml([("empty.bin", 0, [])], [("127.0.0.1", 1)])
+
+
+@pytest.mark.gpu
+def test_verify_cli_resume(tmp_path, oracle):
+    """Flood.cpp:220-299 batched: intact -> all '1'; a flipped byte, a
+    truncated tail and a missing file -> '0' exactly there."""
+    cs = 65536
+    data = oracle.synth(77, 0, 10 * cs + 999)
+    (tmp_path / "f.bin").write_bytes(data.tobytes())
+    assert subprocess.run([ENCODER, "f.bin", "http://127.0.0.1:10101/", "f.flood", "--chunksize", str(cs)],
+                          cwd=tmp_path).returncode == 0
+
+    def verify():
+        out = subprocess.run([VERIFY, "f.flood", "--no-resolve"], cwd=tmp_path, capture_output=True, text=True)
+        assert out.returncode == 0, out.stderr
+        lines = dict(line.split(" ", 1) for line in out.stdout.strip().splitlines())
+        return lines
+
+    r = verify()
+    assert r["f.bin"] == "11 11 " + "1" * 11
+    # content hash: Base64Encode(name + every chunk hash), FloodFile.cpp:324-349
+    hashes = [b64_27(hashlib.sha1(data[i * cs:(i + 1) * cs].tobytes()).digest()) for i in range(11)]
+    want = b64_27(hashlib.sha1(("f.bin" + "".join(hashes)).encode()).digest())
+    assert r["content_hash"] == want
+    assert r["to_download"] == "0"
+
+    bad = data.copy()
+    bad[3 * cs + 5] ^= 0xFF
+    (tmp_path / "f.bin").write_bytes(bad[: 8 * cs + 10].tobytes())  # corrupt chunk 3, cut inside chunk 8
+    r = verify()
+    assert r["f.bin"] == "11 7 " + "111011110" + "00"
+    assert r["to_download"] == "4"
+    os.remove(tmp_path / "f.bin")
+    r = verify()
+    assert r["f.bin"] == "11 0 " + "0" * 11
+
+
+@pytest.mark.gpu
+def test_cpp_api_gpu_suite(tmp_path):
+    out = subprocess.run([os.path.join(LIB, "lbf_gpu_tests"), str(tmp_path)], capture_output=True, text=True)
+    assert out.returncode == 0, out.stderr + out.stdout
+    assert "gpu_tests OK" in out.stdout
