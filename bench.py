@@ -28,6 +28,7 @@ import torch  # noqa: E402  (first: one HIP runtime per process)
 
 from bitflood_amd import DeviceBuffer, b64_27  # noqa: E402
 from bitflood_amd import hashing as H  # noqa: E402
+from bitflood_amd.sharding import max_over_ranks, shard_range  # noqa: E402
 
 GIB = 1 << 30
 SEED_C = 0x5EED
@@ -68,15 +69,6 @@ def barrier(world):
     if world > 1:
         import torch.distributed as dist
         dist.barrier()
-
-
-def max_over_ranks(x, world):
-    if world == 1:
-        return x
-    import torch.distributed as dist
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
 
 
 def traffic_from_profiles(file_bytes):
@@ -164,7 +156,9 @@ def main():
     cs = args.chunk_size
     file_bytes = int(args.file_gib * GIB)
     n_chunks = (file_bytes + cs - 1) // cs
-    stream_start = rank * file_bytes  # this rank's shard of the N x 4 GiB file
+    # this rank's contiguous shard of the N x 4 GiB file (weak scaling)
+    first, last = shard_range(world * n_chunks, rank, world)
+    stream_start = first * cs
 
     buf = DeviceBuffer(file_bytes)
     dig = DeviceBuffer(n_chunks * 20)

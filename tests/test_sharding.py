@@ -1,0 +1,72 @@
+"""Multi-GPU path on CPU: world_size-2 gloo ranks shard a chunk list, hash
+their slices (the oracle stands in for each rank's GPU, since this container
+has none -- the sharding and assembly are what is under test), gather, and
+must equal the single-rank result; the bench's max-over-ranks clock too."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from bitflood_amd.sharding import shard_range
+
+
+def test_shard_range_covers_exactly():
+    for n in [0, 1, 7, 16384, 262144, 262145]:
+        for world in [1, 2, 3, 8]:
+            spans = [shard_range(n, r, world) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            for (b0, e0), (b1, e1) in zip(spans, spans[1:]):
+                assert e0 == b1
+            sizes = [e - b for b, e in spans]
+            assert max(sizes) - min(sizes) <= 1
+    assert shard_range(32768 * 8, 3, 8) == (3 * 32768, 4 * 32768)  # C4: 32,768 chunks per GPU
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, out_dir):
+    import torch.distributed as dist
+
+    from bitflood_amd.sharding import gather_digests, max_over_ranks, shard_range
+    from tests.oracle_lib import Oracle
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    orc = Oracle()
+    cs = 4096
+    size = 77 * cs + 1234  # ragged tail
+    data = orc.synth(0x5EED, 0, size)
+    n = (size + cs - 1) // cs
+    b, e = shard_range(n, rank, world)
+    offs = np.arange(b, e, dtype=np.uint64) * np.uint64(cs)
+    sizes = np.array([min(cs, size - int(o)) for o in offs], dtype=np.uint32)
+    local = orc.sha1_batch(data, offs, sizes)
+    full = gather_digests(local, n, world)
+    t = max_over_ranks(float(rank + 1), world)
+    np.save(os.path.join(out_dir, f"r{rank}.npy"), full)
+    with open(os.path.join(out_dir, f"t{rank}.txt"), "w") as f:
+        f.write(str(t))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2])
+def test_gloo_two_ranks_gather_equals_single(tmp_path, oracle, world):
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    cs = 4096
+    size = 77 * cs + 1234
+    data = oracle.synth(0x5EED, 0, size)
+    want = oracle.encode_buffer(data, cs)
+    for r in range(world):
+        got = np.load(tmp_path / f"r{r}.npy")
+        assert np.array_equal(got, want)
+        assert float((tmp_path / f"t{r}.txt").read_text()) == float(world)
