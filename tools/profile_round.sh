@@ -12,10 +12,11 @@ REPO=${GRAFT_REPO_ROOT:-/root/repo}
 OUT=$REPO/gpurun_out/prof/$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
+# trace pass: the bench command exactly as the driver runs it (default flags)
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o trace --output-format csv \
+  -- python3 "$REPO/bench.py" $* > "$OUT/trace.log" 2>&1 || { echo "trace run failed rc=$?"; tail -20 "$OUT/trace.log"; exit 1; }
+# counter passes: same workload, fewer steps, no CPU leg
 BENCH="$REPO/bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-e2e $*"
-
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o trace --output-format csv \
-  -- python3 $BENCH > "$OUT/trace.log" 2>&1 || { echo "trace run failed rc=$?"; tail -20 "$OUT/trace.log"; exit 1; }
 
 timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY \
   SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE \
