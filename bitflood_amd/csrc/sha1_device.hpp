@@ -151,6 +151,71 @@ __device__ __forceinline__ void expand_store(uint32_t (&w)[16], uint4* out, int 
   }
 }
 
+// Round constant of round i (sha.cpp:43-78).
+__host__ __device__ constexpr uint32_t round_k(int i) {
+  return i < 20 ? kK1 : (i < 40 ? kK2 : (i < 60 ? kK3 : kK4));
+}
+
+// A round whose schedule word already carries the round constant (wk = W[i] +
+// K[i], added by the producer).  The remaining four-term sum is one VOP2 add and
+// one v_add3_u32: a lone wave then issues the round's five VALU ops back to back
+// (≈20.4 cycles), while the two-add3 form stalls ≈5 cycles per round on gfx950
+// (tools/gen_round_order.py).
+__device__ __forceinline__ void round_step_wk(int i, uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d,
+                                              uint32_t& e, uint32_t wk) {
+  uint32_t f;
+  if (i < 20) f = f_choose(b, c, d);
+  else if (i < 40 || i >= 60) f = f_parity(b, c, d);
+  else f = f_major(b, c, d);
+  const uint32_t s = e + wk;
+  const uint32_t n = rotl(a, 5) + f + s;
+  e = d;
+  d = c;
+  c = rotl(b, 30);
+  b = a;
+  a = n;
+}
+
+__device__ __forceinline__ void compress_expanded_wk(Digest& s, const uint4* w, int stride) {
+  uint32_t a = s.h[0], b = s.h[1], c = s.h[2], d = s.h[3], e = s.h[4];
+#pragma unroll
+  for (int q = 0; q < 20; ++q) {
+    const uint4 v = w[q * stride];
+    round_step_wk(4 * q + 0, a, b, c, d, e, v.x);
+    round_step_wk(4 * q + 1, a, b, c, d, e, v.y);
+    round_step_wk(4 * q + 2, a, b, c, d, e, v.z);
+    round_step_wk(4 * q + 3, a, b, c, d, e, v.w);
+  }
+  s.h[0] += a;
+  s.h[1] += b;
+  s.h[2] += c;
+  s.h[3] += d;
+  s.h[4] += e;
+}
+
+// Half (kHalf = 0: words 0..39, 1: words 40..79) of the 80-word schedule with
+// the round constants added, stored as 10 uint4 `stride` apart.  `w` is the
+// 16-word rolling window and carries over from half 0 to half 1.
+template <int kHalf>
+__device__ __forceinline__ void expand_store_wk(uint32_t (&w)[16], uint4* out, int stride) {
+#pragma unroll
+  for (int q = 10 * kHalf; q < 10 * kHalf + 10; ++q) {
+    uint32_t x[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = 4 * q + j;
+      if (i < 16) {
+        x[j] = w[i];
+      } else {
+        x[j] = sched(w[(i + 13) & 15], w[(i + 8) & 15], w[(i + 2) & 15], w[i & 15]);
+        w[i & 15] = x[j];
+      }
+      x[j] += round_k(i);
+    }
+    out[q * stride] = make_uint4(x[0], x[1], x[2], x[3]);
+  }
+}
+
 // Big-endian block from four 16-byte little-endian vectors.
 __device__ __forceinline__ void block_from_vec(uint32_t (&w)[16], const uint4& q0, const uint4& q1,
                                                const uint4& q2, const uint4& q3) {

@@ -10,9 +10,12 @@
 // keeps its chain state and the 16-word schedule in VGPRs, streams its chunk
 // with 16-byte global loads two blocks ahead of use, and finishes the 0x80/
 // length padding in registers.  See DESIGN.md for the roofline discussion.
+// Kernel "pc" (variant 2): producer/consumer split for few chains.
+// Kernel "lds" (variant 3): variant 1 with LDS-DMA staging, for many chains.
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <mutex>
 
 #include "lbf_internal.hpp"
 #include "sha1_device.hpp"
@@ -139,7 +142,11 @@ __device__ unsigned long long g_pc_stamps[8192 * 8];
     __builtin_amdgcn_sched_barrier(0);                                                \
   } while (0)
 #define PC_ACC(slot, a, b) acc[slot] += (b) - (a)
+#define PC_COPY(dst, src) dst = src
 #else
+#define PC_COPY(dst, src) \
+  do {                    \
+  } while (0)
 #define PC_STAMP(var) \
   do {                \
   } while (0)
@@ -319,6 +326,209 @@ __global__ void __launch_bounds__(128) sha1_pc_kernel(ChunkParams p) {
 #endif
 }
 
+// ---------------------------------------------------------------------------
+// Kernel "pc2" (variant 4): one consumer, TWO producers per 64 chains.
+//
+// The consumer's round is cheapest (five VALU ops issued back to back) when
+// its schedule word already carries the round constant, leaving one v_add_u32
+// and one v_add3_u32 for the sum.  Adding K costs the producer 80 more ops per
+// block, more than one producer wave has to spare, so two producers alternate
+// blocks: producer X builds steps X, X+2, X+4, ... and spends two barrier
+// intervals on each (words 0..39 before the first, 40..79 before the second).
+// W ring: 3 slots (step k in slot k % 3): a slot is rewritten only after the
+// consumer has passed the barrier that ends its read.  Raw staging: 2 slots of
+// 4 KiB per producer.  LDS 76 KiB -> two workgroups per CU.
+// ---------------------------------------------------------------------------
+constexpr int kP2Ring = 3;
+constexpr int kP2Raw = 2;  // raw slots per producer
+constexpr int kP2LdsBytes = (kP2Ring * kPcSlotU4 + 2 * kP2Raw * kPcRawU4) * 16;
+
+// Raw bytes of `step` into raw slot `slot` of this producer: 4 DMA ops always.
+__device__ __forceinline__ void p2_dma(const ChainInfo& c, uint32_t step, uint32_t raw_lds, uint32_t slot) {
+  const bool ok = c.aligned && step < c.nfull;
+  const uint8_t* src = ok ? c.src + 64ull * step : reinterpret_cast<const uint8_t*>(g_pc_dummy);
+  const uint32_t base = raw_lds + slot * (kPcRawU4 * 16);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) dma16(src + 16 * j, base + j * (kPcLanes * 16));
+}
+
+// The 16 message words of `step`: full blocks from the raw slot (aligned) or
+// global memory (misaligned), final blocks built from the tail.
+__device__ __forceinline__ void p2_block(uint32_t (&w)[16], const uint4* raw, const ChainInfo& c, uint32_t step) {
+  if (step < c.nfull) {
+    if (c.aligned) {
+      block_from_vec(w, raw[0], raw[kPcLanes], raw[2 * kPcLanes], raw[3 * kPcLanes]);
+    } else {
+      load_words_any(w, c.src + 64ull * step, 64);
+#pragma unroll
+      for (int k = 0; k < 16; ++k) w[k] = bswap(w[k]);
+    }
+  } else {
+    final_block(w, c.src + 64ull * c.nfull, c.size & 63u, c.size, step != c.nfull);
+  }
+}
+
+template <bool kUniform>
+__global__ void __launch_bounds__(192) sha1_pc2_kernel(ChunkParams p) {
+  extern __shared__ __attribute__((aligned(16))) uint4 ring[];  // W[3][20][64] | raw[2][2][4][64]
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t i = blockIdx.x * kPcLanes + lane;
+  const ChainInfo c = chain_info<kUniform>(p, i);
+  const uint32_t nsteps = __builtin_amdgcn_readfirstlane(wave_max(c.total));
+#ifdef LBF_PC_STAMPS
+  unsigned long long acc[4] = {0, 0, 0, 0}, t0 = 0, t1 = 0, t2 = 0, t3 = 0;
+#endif
+
+  if (wave != 0) {
+    // ---------------- producer X = wave - 1: steps X, X+2, ... ----------------
+    const uint32_t X = wave - 1;
+    uint4* raw = ring + kP2Ring * kPcSlotU4 + X * (kP2Raw * kPcRawU4);
+    const uint32_t raw_lds = (uint32_t)reinterpret_cast<uintptr_t>(raw);
+    p2_dma(c, X, raw_lds, 0);
+    p2_dma(c, X + 2, raw_lds, 1);
+    uint32_t w[16];
+    // Interval b ends at barrier b.  Producer X finishes step b when b % 2 == X
+    // and starts step b + 1 otherwise; producer 0 builds step 0 whole.
+    for (uint32_t b = 0; b < nsteps; ++b) {
+      const bool second = (b & 1u) == X;
+      const uint32_t step = second ? b : b + 1;
+      const bool first_too = (b == 0 && X == 0);
+      PC_STAMP(t0);
+      PC_COPY(t1, t0);
+      if ((!second || first_too) && step < nsteps) {
+        const uint32_t j = (step - X) >> 1;  // this producer's j-th step
+        // block j has landed once only block j+1's 4 DMAs may be pending
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        PC_STAMP(t1);
+        p2_block(w, raw + (j & 1u) * kPcRawU4 + lane, c, step);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // raw slot read before it is refilled
+        p2_dma(c, step + 4, raw_lds, j & 1u);
+        expand_store_wk<0>(w, ring + (step % kP2Ring) * kPcSlotU4 + lane, kPcLanes);
+      }
+      if (second && step < nsteps) expand_store_wk<1>(w, ring + (step % kP2Ring) * kPcSlotU4 + lane, kPcLanes);
+      PC_STAMP(t2);
+      __syncthreads();  // barrier b
+      PC_STAMP(t3);
+      PC_ACC(0, t0, t1);
+      PC_ACC(1, t1, t2);
+      PC_ACC(2, t2, t3);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA outlives the workgroup
+  } else {
+    // ---------------- consumer ----------------
+    Digest s;
+    s.init();
+    for (uint32_t k = 0; k < nsteps; ++k) {
+      PC_STAMP(t0);
+      __syncthreads();  // barrier k: slot k % 3 complete
+      PC_STAMP(t1);
+      if (k < c.total) compress_expanded_wk(s, ring + (k % kP2Ring) * kPcSlotU4 + lane, kPcLanes);
+      PC_STAMP(t2);
+      PC_ACC(0, t0, t1);
+      PC_ACC(1, t1, t2);
+    }
+    if (i < p.n) {
+      uint32_t be[5];
+#pragma unroll
+      for (int k = 0; k < 5; ++k) be[k] = bswap(s.h[k]);
+      if (p.digests) {
+        uint32_t* o = reinterpret_cast<uint32_t*>(p.digests + 20ull * i);
+#pragma unroll
+        for (int k = 0; k < 5; ++k) o[k] = be[k];
+      }
+      if (p.verdicts) {
+        const uint32_t* e = reinterpret_cast<const uint32_t*>(p.expected + 20ull * i);
+        uint32_t diff = 0;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) diff |= be[k] ^ e[k];
+        p.verdicts[i] = diff == 0 ? 1 : 0;
+      }
+    }
+  }
+#ifdef LBF_PC_STAMPS
+  if (lane == 0) {
+    unsigned long long* o = g_pc_stamps + (blockIdx.x * 3 + wave) * 4;
+    o[0] = acc[0];
+    o[1] = acc[1];
+    o[2] = acc[2];
+    o[3] = nsteps;
+  }
+#endif
+}
+
+// ---------------------------------------------------------------------------
+// Kernel "lds" (variant 3): one chunk per lane for MANY chains.
+//
+// With >= 4 waves per SIMD the VALU itself is the limit (≈2,040 SIMD cycles per
+// 64-byte block) and what is left to win is memory stall: in the
+// lane kernel the compiler sinks every 16-byte load next to its use, so each
+// block waits a full HBM round trip.  Here each wave streams its 64 chains'
+// next kStages blocks global -> LDS with DMA (no VGPRs in flight, so the
+// compiler cannot move them) and waits by count.  LDS per wave: kStages x 4 KiB.
+// ---------------------------------------------------------------------------
+template <int kStages>
+__device__ __forceinline__ void lds_dma_step(const ChainInfo& c, uint32_t step, uint32_t wave_lds) {
+  const bool ok = c.aligned && step < c.nfull;
+  const uint8_t* src = ok ? c.src + 64ull * step : reinterpret_cast<const uint8_t*>(g_pc_dummy);
+  const uint32_t slot = wave_lds + (step % kStages) * (kPcRawU4 * 16);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) dma16(src + 16 * j, slot + j * (kPcLanes * 16));
+}
+
+template <bool kUniform, int kStages>
+__global__ void __launch_bounds__(256) sha1_lds_kernel(ChunkParams p) {
+  extern __shared__ __attribute__((aligned(16))) uint4 stage[];  // [wave][kStages][4][64]
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const ChainInfo c = chain_info<kUniform>(p, i);
+  uint4* mine = stage + wave * (kStages * kPcRawU4);
+  const uint32_t wave_lds = (uint32_t)reinterpret_cast<uintptr_t>(mine);
+  const uint32_t nsteps = __builtin_amdgcn_readfirstlane(wave_max(c.nfull));
+  const bool any_unaligned = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(__ballot(c.total != 0 && !c.aligned) != 0));
+  Digest s;
+  s.init();
+#pragma unroll
+  for (uint32_t k = 0; k < (uint32_t)kStages; ++k) lds_dma_step<kStages>(c, k, wave_lds);
+  for (uint32_t k = 0; k < nsteps; ++k) {
+    // block k has landed once at most the (kStages-1) younger steps are pending
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (kStages - 1)) : "memory");
+    const uint4* raw = mine + (k % kStages) * kPcRawU4 + lane;
+    uint32_t w[16];
+    block_from_vec(w, raw[0], raw[kPcLanes], raw[2 * kPcLanes], raw[3 * kPcLanes]);
+    if (any_unaligned && !c.aligned && k < c.nfull) {
+      load_words_any(w, c.src + 64ull * k, 64);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) w[q] = bswap(w[q]);
+    }
+    // the slot is refilled below: its ds_reads must have returned first
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    lds_dma_step<kStages>(c, k + kStages, wave_lds);
+    if (k < c.nfull) compress(s, w);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA outlives the wave
+  if (i >= p.n) return;
+  finish(s, c.src + 64ull * c.nfull, c.size & 63u, c.size);
+  uint32_t be[5];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) be[k] = bswap(s.h[k]);
+  if (p.digests) {
+    uint32_t* o = reinterpret_cast<uint32_t*>(p.digests + 20ull * i);
+#pragma unroll
+    for (int k = 0; k < 5; ++k) o[k] = be[k];
+  }
+  if (p.verdicts) {
+    const uint32_t* e = reinterpret_cast<const uint32_t*>(p.expected + 20ull * i);
+    uint32_t diff = 0;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) diff |= be[k] ^ e[k];
+    p.verdicts[i] = diff == 0 ? 1 : 0;
+  }
+}
+constexpr int kLdsStages = 2;
+
 // Counter-mode splitmix64 fill, 16 bytes per thread per step.
 __global__ void __launch_bounds__(256) fill_synth_kernel(uint8_t* dst, uint64_t len, uint64_t seed,
                                                          uint64_t start_word) {
@@ -357,14 +567,32 @@ int launch_chunks(const ChunkParams& p, hipStream_t stream) {
   if (variant == 0) {
     // Few chains: the per-chain instruction count bounds the time, so split the
     // schedule off to producer waves.  Many chains: every SIMD is busy and the
-    // fused one-chunk-per-lane kernel issues the fewest instructions in total.
-    variant = p.n <= kPcMaxChains ? 2 : 1;
+    // fused one-chunk-per-lane kernel issues the fewest instructions in total;
+    // its LDS-staged form (3) measured equal or faster than the register form
+    // (1) at every point of tools/sweep_variants.py (profiles/r01/sweep_v123.log).
+    variant = p.n <= kPcMaxChains ? 2 : 3;
   }
   if (variant == 2) {
     const uint32_t blocks = (p.n + kPcLanes - 1) / kPcLanes;
     constexpr int lds = pc_lds_bytes<2>();
     if (p.offsets) hipLaunchKernelGGL((sha1_pc_kernel<false, 2>), dim3(blocks), dim3(128), lds, stream, p);
     else hipLaunchKernelGGL((sha1_pc_kernel<true, 2>), dim3(blocks), dim3(128), lds, stream, p);
+  } else if (variant == 4) {
+    static std::once_flag once;
+    std::call_once(once, [] {
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc2_kernel<false>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, kP2LdsBytes);
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc2_kernel<true>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, kP2LdsBytes);
+    });
+    const uint32_t blocks = (p.n + kPcLanes - 1) / kPcLanes;
+    if (p.offsets) hipLaunchKernelGGL(sha1_pc2_kernel<false>, dim3(blocks), dim3(192), kP2LdsBytes, stream, p);
+    else hipLaunchKernelGGL(sha1_pc2_kernel<true>, dim3(blocks), dim3(192), kP2LdsBytes, stream, p);
+  } else if (variant == 3) {
+    const uint32_t blocks = (p.n + 255) / 256;
+    constexpr int lds = 4 * kLdsStages * kPcRawU4 * 16;
+    if (p.offsets) hipLaunchKernelGGL((sha1_lds_kernel<false, kLdsStages>), dim3(blocks), dim3(256), lds, stream, p);
+    else hipLaunchKernelGGL((sha1_lds_kernel<true, kLdsStages>), dim3(blocks), dim3(256), lds, stream, p);
   } else {
     // 64-thread workgroups while waves are scarce so they spread over every CU.
     const uint32_t threads = p.n <= 65536u ? 64u : 256u;
@@ -436,7 +664,7 @@ extern "C" int lbf_sha1_uniform_launch(const uint8_t* d_base, uint64_t len, uint
 }
 
 extern "C" int lbf_set_kernel_variant(int variant) {
-  if (variant < 0 || variant > 2) return fail(LBF_ERR_INVALID, "unknown kernel variant");
+  if (variant < 0 || variant > 4) return fail(LBF_ERR_INVALID, "unknown kernel variant");
   lbf::g_variant.store(variant);
   return LBF_OK;
 }

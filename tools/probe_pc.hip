@@ -19,22 +19,24 @@ static void run(int variant, uint8_t* buf, uint64_t len, uint32_t cs, uint8_t* d
     return;
   }
   const int wgs = (int)((n + 63) / 64);
-  std::vector<unsigned long long> h(wgs * 8);
-  hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(lbf::g_pc_stamps), wgs * 8 * 8, 0, hipMemcpyDeviceToHost);
-  double a[2][3] = {{0}};
+  const int nw = variant == 4 ? 3 : 2;  // waves per workgroup
+  std::vector<unsigned long long> h(wgs * nw * 4);
+  hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(lbf::g_pc_stamps), wgs * nw * 4 * 8, 0, hipMemcpyDeviceToHost);
+  double a[3][3] = {{0}};
   double steps = 0;
   for (int w = 0; w < wgs; ++w)
-    for (int r = 0; r < 2; ++r) {
-      for (int j = 0; j < 3; ++j) a[r][j] += (double)h[(w * 2 + r) * 4 + j];
-      if (r == 0) steps += (double)h[(w * 2) * 4 + 3];
+    for (int r = 0; r < nw; ++r) {
+      for (int j = 0; j < 3; ++j) a[r][j] += (double)h[(w * nw + r) * 4 + j];
+      if (r == 0) steps += (double)h[(w * nw) * 4 + 3];
     }
   steps /= wgs;
-  for (int r = 0; r < 2; ++r)
+  for (int r = 0; r < nw; ++r)
     for (int j = 0; j < 3; ++j) a[r][j] /= wgs * steps;
-  printf("variant %d cs=%u n=%lu: %.3f ms (%.1f GiB/s)  steps=%.0f  cycles/step: consumer[wait %.0f work %.0f] "
-         "producer[vmwait %.0f work %.0f barrier %.0f]\n",
-         variant, cs, (unsigned long)n, ms, len / (ms * 1e-3) / (1 << 30), steps, a[0][0], a[0][1], a[1][0],
-         a[1][1], a[1][2]);
+  printf("variant %d cs=%u n=%lu: %.3f ms (%.1f GiB/s)  steps=%.0f  cycles/step: consumer[wait %.0f work %.0f]",
+         variant, cs, (unsigned long)n, ms, len / (ms * 1e-3) / (1 << 30), steps, a[0][0], a[0][1]);
+  for (int r = 1; r < nw; ++r)
+    printf(" producer%d[vmwait %.0f work %.0f barrier %.0f]", r - 1, a[r][0], a[r][1], a[r][2]);
+  printf("\n");
 }
 
 int main() {
@@ -44,7 +46,7 @@ int main() {
   hipMalloc(&dig, (len / 65536) * 20);
   lbf_fill_synthetic(buf, len, 0x5EED, 0, nullptr);
   hipDeviceSynchronize();
-  for (int v : {2}) {
+  for (int v : {2, 4}) {
     run(v, buf, len, 262144, dig);
     run(v, buf, len / 2, 262144, dig);
     run(v, buf, len, 1 << 20, dig);

@@ -8,6 +8,7 @@ shape (32 GiB at 1 MiB = 32,768 chunks).  Prints one JSON line per point.
 Usage: python tools/sweep_variants.py [--max-gib 64] [--reps 3]
 """
 import argparse
+import hashlib
 import ctypes
 import json
 import os
@@ -29,7 +30,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--max-gib", type=int, default=64)
     ap.add_argument("--reps", type=int, default=3)
-    ap.add_argument("--variants", default="1,2")
+    ap.add_argument("--variants", default="1,2,3")
     a = ap.parse_args()
     size = a.max_gib * GIB
     buf = DeviceBuffer(size)
@@ -43,15 +44,19 @@ def main():
     for cs, n in points:
         if n * cs > size:
             continue
+        ref = None
         for v in [int(x) for x in a.variants.split(",")]:
             H.set_kernel_variant(v)
             ms = ctypes.c_float()
             check(lib.lbf_time_uniform(buf.ptr, n * cs, cs, 0, n, dig.ptr, 1, None, ctypes.byref(ms)))  # warm
             check(lib.lbf_time_uniform(buf.ptr, n * cs, cs, 0, n, dig.ptr, a.reps, None, ctypes.byref(ms)))
             gbs = n * cs / (ms.value * 1e-3) / 1e9
+            dd = hashlib.sha1(dig.download(n * 20).tobytes()).hexdigest()
+            ref = ref or dd
             print(json.dumps({"chunk_size": cs, "chunks": n, "gib": n * cs / GIB, "variant": v,
                               "ms": round(ms.value, 4), "GB/s": round(gbs, 1),
-                              "GiB/s": round(gbs * 1e9 / GIB, 1), "hbm_frac": round(gbs / 8000, 4)}),
+                              "GiB/s": round(gbs * 1e9 / GIB, 1), "hbm_frac": round(gbs / 8000, 4),
+                              "digests_agree": dd == ref}),
                   flush=True)
     H.set_kernel_variant(0)
     buf.free()
