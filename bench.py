@@ -33,6 +33,16 @@ from bitflood_amd.sharding import max_over_ranks, shard_range  # noqa: E402
 GIB = 1 << 30
 SEED_C = 0x5EED
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak, MI355X_MICROARCH.md "Chip-level parameters"
+CLOCK_HZ = 2.4e9       # MI355X max engine clock, MI355X_MICROARCH.md (chip table)
+N_SIMDS = 1024         # 256 CUs x 4 SIMDs
+# kernel variant -> uniform-mode kernel symbol (profiles/pmc_traffic.json "kernel")
+KERNELS = {1: "sha1_lane_kernel<true>", 2: "sha1_pc_kernel<true, 2>", 3: "sha1_lds_kernel<true, 2>",
+           4: "sha1_pc2_kernel<true>"}
+# Measured issue floors per 64-byte block (tools/gen_round_order.py):
+#  pc2 consumer: 80 rounds x (5 VALU at 4.09 cycles + a quarter ds_read_b128 at 16 cycles)
+#  fused lane/lds: 613 VALU; a lone wave issues one per 4.09 cycles, a SIMD retires one per 4
+PC2_CYCLES_PER_BLOCK = 80 * (5 * 4.09 + 4.0)
+FUSED_VALU_PER_BLOCK = 613
 
 
 def parse():
@@ -71,14 +81,15 @@ def barrier(world):
         dist.barrier()
 
 
-def traffic_from_profiles(file_bytes):
+def traffic_from_profiles(file_bytes, kernel):
     """HBM bytes per launch measured with rocprofv3 PMC (FETCH_SIZE x2, gfx950
-    correction), recorded by tools/pmc_traffic.py."""
+    correction), recorded by tools/pmc_traffic.py for this
+    workload size and this kernel."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(p) as f:
             d = json.load(f)
-        if int(d.get("file_bytes", -1)) == int(file_bytes):
+        if int(d.get("file_bytes", -1)) == int(file_bytes) and kernel in d.get("kernel", ""):
             return float(d["hbm_bytes_per_launch"])
     except Exception:
         pass
@@ -133,6 +144,17 @@ def _host_desc():
     except Exception:
         pass
     return {"cpu_model": model, "os_cpu_count": os.cpu_count()}
+
+
+def compute_floor_ms(variant, cs, n_chunks):
+    """Lower bound on one launch from instruction issue alone (SHA-1 is a serial
+    chain per chunk, so few chunks are bound by one chain's issue rate)."""
+    blocks = (cs + 9 + 63) // 64  # compressions per chunk incl. padding
+    if variant == 4:
+        return blocks * PC2_CYCLES_PER_BLOCK / CLOCK_HZ * 1e3
+    chain = blocks * FUSED_VALU_PER_BLOCK * 4.09 / CLOCK_HZ
+    chip = n_chunks / 64 * blocks * FUSED_VALU_PER_BLOCK * 4.0 / (N_SIMDS * CLOCK_HZ)
+    return max(chain, chip) * 1e3
 
 
 def e2e_rate(host_data, cs):
@@ -196,6 +218,8 @@ def main():
     achieved_gbs = file_bytes / launch_s / 1e9
 
     digests = dig.download(n_chunks * 20).reshape(n_chunks, 20)
+    variant = H.load().lbf_kernel_for(n_chunks)
+    floor_ms = compute_floor_ms(variant, cs, n_chunks)
     out = None
     if rank == 0:
         out = {
@@ -218,7 +242,7 @@ def main():
                 "file_bytes_per_gpu": file_bytes,
                 "chunk_size": cs,
                 "chunks_per_gpu": n_chunks,
-                "kernel_variant": H.load().lbf_get_kernel_variant(),
+                "kernel": KERNELS.get(variant, str(variant)),
                 "parallelism": f"chunk-shard x{world} (no data-path collective)",
             },
             "roofline": {
@@ -227,9 +251,17 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
-                "traffic": traffic_from_profiles(file_bytes),
+                "traffic": traffic_from_profiles(file_bytes, KERNELS.get(variant, "?")),
                 "kernel_ms": round(launch_s * 1e3, 4),
                 "algorithmic_bytes_per_launch": file_bytes,
+            },
+            # SHA-1 is integer VALU work on a serial chain per chunk: the binding
+            # limit is instruction issue, not HBM.
+            "compute_floor": {
+                "bound": "per-chain issue" if variant in (2, 4) else "valu",
+                "floor_ms": round(floor_ms, 4),
+                "frac": round(floor_ms / (launch_s * 1e3), 4),
+                "clock_ghz": CLOCK_HZ / 1e9,
             },
             "digest_check": hashlib.sha1(digests.tobytes()).hexdigest(),
         }

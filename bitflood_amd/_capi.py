@@ -58,6 +58,7 @@ _SIGS = {
                                            _c.c_void_p]),
     "lbf_set_kernel_variant": (_c.c_int, [_c.c_int]),
     "lbf_get_kernel_variant": (_c.c_int, []),
+    "lbf_kernel_for": (_c.c_int, [_c.c_uint64]),
     "lbf_fill_synthetic": (_c.c_int, [_c.c_void_p, _c.c_uint64, _c.c_uint64, _c.c_uint64, _c.c_void_p]),
     "lbf_dev_malloc": (_c.c_int, [_c.POINTER(_c.c_void_p), _c.c_uint64]),
     "lbf_dev_free": (_c.c_int, [_c.c_void_p]),

@@ -35,6 +35,7 @@ struct ChunkParams {
   uint8_t* verdicts;         // n bytes or null
 };
 
+int pick_variant(uint64_t n);
 int launch_chunks(const ChunkParams& p, hipStream_t stream);
 
 }  // namespace lbf

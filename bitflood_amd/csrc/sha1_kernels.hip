@@ -12,6 +12,7 @@
 // length padding in registers.  See DESIGN.md for the roofline discussion.
 // Kernel "pc" (variant 2): producer/consumer split for few chains.
 // Kernel "lds" (variant 3): variant 1 with LDS-DMA staging, for many chains.
+// Kernel "pc2" (variant 4): one consumer + two producers, W+K hand-over, for few chains.
 #include <hip/hip_runtime.h>
 
 #include <atomic>
@@ -561,17 +562,23 @@ constexpr uint32_t kPcMaxChains = 32768;
 
 }  // namespace
 
-int launch_chunks(const ChunkParams& p, hipStream_t stream) {
-  if (p.n == 0) return LBF_OK;
+int pick_variant(uint64_t n) {
   int variant = g_variant.load();
   if (variant == 0) {
-    // Few chains: the per-chain instruction count bounds the time, so split the
-    // schedule off to producer waves.  Many chains: every SIMD is busy and the
-    // fused one-chunk-per-lane kernel issues the fewest instructions in total;
-    // its LDS-staged form (3) measured equal or faster than the register form
-    // (1) at every point of tools/sweep_variants.py (profiles/r01/sweep_v123.log).
-    variant = p.n <= kPcMaxChains ? 2 : 3;
+    // Few chains: the per-chain instruction count bounds the time, so the
+    // schedule (with the round constants folded in) comes from two producer
+    // waves (4).  Many chains: every SIMD is busy and the fused one-chunk-per-lane
+    // kernel issues the fewest instructions in total; its LDS-staged form (3)
+    // measured equal or faster than the register form (1) at every point of
+    // tools/sweep_variants.py (profiles/r01/sweep_v123.log, sweep_v24.log).
+    variant = n <= kPcMaxChains ? 4 : 3;
   }
+  return variant;
+}
+
+int launch_chunks(const ChunkParams& p, hipStream_t stream) {
+  if (p.n == 0) return LBF_OK;
+  const int variant = pick_variant(p.n);
   if (variant == 2) {
     const uint32_t blocks = (p.n + kPcLanes - 1) / kPcLanes;
     constexpr int lds = pc_lds_bytes<2>();
@@ -670,6 +677,8 @@ extern "C" int lbf_set_kernel_variant(int variant) {
 }
 
 extern "C" int lbf_get_kernel_variant(void) { return lbf::g_variant.load(); }
+
+extern "C" int lbf_kernel_for(uint64_t n_chunks) { return lbf::pick_variant(n_chunks); }
 
 extern "C" int lbf_fill_synthetic(uint8_t* d_buf, uint64_t len, uint64_t seed, uint64_t start, void* stream) {
   if (len == 0) return LBF_OK;

@@ -121,10 +121,13 @@ int lbf_sha1_launch(const uint8_t* d_base, const uint64_t* d_offsets,
 int lbf_sha1_uniform_launch(const uint8_t* d_base, uint64_t len, uint32_t chunk_size,
                             uint64_t first_chunk, uint64_t n, uint8_t* d_digests,
                             const uint8_t* d_expected, uint8_t* d_verdicts, void* stream);
-/* Kernel variant selection for the two launchers above (0 = automatic).
- * Exposed for benchmarking and tests; see DESIGN.md "kernels". */
+/* Kernel variant selection for the two launchers above (0 = automatic):
+ * 1 lane, 2 pc, 3 lds, 4 pc2.  Exposed for benchmarking and tests; see
+ * DESIGN.md "kernels".  lbf_kernel_for(n) is the variant a launch of n
+ * chunks runs under the current setting. */
 int lbf_set_kernel_variant(int variant);
 int lbf_get_kernel_variant(void);
+int lbf_kernel_for(uint64_t n_chunks);
 
 /* Synthetic bytes (counter-mode splitmix64): fill
  * d_buf[0..len) with stream `seed` starting at stream byte `start`
