@@ -167,9 +167,13 @@ class DeviceBuffer:
         check(load().lbf_memcpy_d2h(out.ctypes.data, self.ptr + offset, nbytes))
         return out.view(dtype)
 
-    def fill_synthetic(self, seed: int, start: int = 0, nbytes: int | None = None, stream=None):
-        nbytes = self.nbytes if nbytes is None else nbytes
-        check(load().lbf_fill_synthetic(self.ptr, nbytes, seed, start, stream))
+    def fill_synthetic(self, seed: int, start: int = 0, nbytes: int | None = None, stream=None, offset: int = 0):
+        """Bytes [start, start+nbytes) of synthetic stream `seed` into this
+        buffer at byte `offset` (16-byte aligned)."""
+        nbytes = self.nbytes - offset if nbytes is None else nbytes
+        if offset < 0 or offset + nbytes > self.nbytes:
+            raise ValueError("fill_synthetic: range outside the buffer")
+        check(load().lbf_fill_synthetic(self.ptr + offset, nbytes, seed, start, stream))
 
 
 def uniform_launch(base: DeviceBuffer | int, length: int, chunk_size: int, first: int, n: int,

@@ -83,6 +83,64 @@ def chunk_digests(data, chunk_size):
     return out
 
 
+def stream_digests(lib, seed, start, size, cs, slab=256 << 20, workers=None):
+    """Raw SHA-1 digests of every cs-byte chunk of stream `seed` bytes
+    [start, start+size), slab-parallel (ctypes and hashlib release the GIL)."""
+    from concurrent.futures import ThreadPoolExecutor
+    assert slab % cs == 0 and size % cs == 0
+
+    def one(s0):
+        ln = min(slab, size - s0)
+        buf = np.empty(ln, dtype=np.uint8)
+        lib.oracle_synth_fill_mt(buf.ctypes.data, ln, seed, start + s0, 1)
+        mv = memoryview(buf)
+        return [hashlib.sha1(mv[j:j + cs]).digest() for j in range(0, ln, cs)]
+
+    with ThreadPoolExecutor(max_workers=workers or os.cpu_count() or 1) as ex:
+        parts = list(ex.map(one, range(0, size, slab)))
+    return [d for part in parts for d in part]
+
+
+def dod(digests):
+    h = hashlib.sha1()
+    for d in digests:
+        h.update(d)
+    return h.hexdigest()
+
+
+def big(lib):
+    """C3 and C4 at full size: digest-of-digests per file /
+    per 8-GPU shard plus sampled chunk strings."""
+    gib = 1 << 30
+    cs = 262144
+    files, allh = [], hashlib.sha1()
+    for f in range(64):
+        d = stream_digests(lib, f, 0, gib, cs)
+        for x in d:
+            allh.update(x)
+        files.append({"seed": f, "n_chunks": len(d), "sha1_of_concat_raw_digests_hex": dod(d),
+                      "first_b64": b64_27(d[0]), "last_b64": b64_27(d[-1])})
+        print(f"  C3 file {f}", end="\r", file=sys.stderr)
+    write("c3.json", {
+        "config": "C3: 64 files x 1 GiB (file f = stream seed f from byte 0), 256 KiB chunks",
+        "file_size": gib, "chunk_size": cs, "files": files,
+        "sha1_of_all_digests_in_file_order_hex": allh.hexdigest(),
+    })
+    cs = 1 << 20
+    shard = 32 * gib
+    shards = []
+    for r in range(8):
+        d = stream_digests(lib, SEED_C, r * shard, shard, cs)
+        shards.append({"rank": r, "first_chunk": r * (shard // cs), "n_chunks": len(d),
+                       "sha1_of_concat_raw_digests_hex": dod(d),
+                       "samples_b64": {str(i): b64_27(d[i]) for i in (0, 1, 12345, len(d) - 1)}})
+        print(f"  C4 shard {r}", end="\r", file=sys.stderr)
+    write("c4.json", {
+        "config": "C4: one 256 GiB file (stream seed 0x5EED), 1 MiB chunks, 8 contiguous shards of 32 GiB",
+        "seed": SEED_C, "size": 8 * shard, "chunk_size": cs, "shards": shards,
+    })
+
+
 def write(name, obj):
     with open(os.path.join(HERE, name), "w") as f:
         json.dump(obj, f, indent=1, sort_keys=True)
@@ -197,4 +255,7 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if "--big" in sys.argv:
+        big(load_oracle())
+    else:
+        main()
