@@ -6,6 +6,8 @@
 #include <unistd.h>
 
 #include <cstdio>
+#include <map>
+#include <vector>
 
 #include "lbf_hash.h"
 #include "libBitFlood/Encoder.H"
@@ -22,6 +24,8 @@ bool decode_hash(const std::string& s, U8* out) {
 }
 
 }  // namespace
+
+lbf_ctx* Flood::Ctx() const { return m_ctx ? m_ctx : Encoder::Context(); }
 
 std::string Flood::PathOf(const std::string& i_name) const {
   if (m_rootdir.empty() || (!i_name.empty() && i_name[0] == '/')) return i_name;
@@ -41,7 +45,7 @@ Error::ErrorCode Flood::SetupFilesAndChunks() {
   m_runtimefiles.clear();
   m_chunkstodownload.clear();
   if (!m_floodfile) return Error::UNKNOWN_ERROR_LBF;
-  lbf_ctx* ctx = Encoder::Context();
+  lbf_ctx* ctx = Ctx();
   if (!ctx) return Error::UNKNOWN_ERROR_LBF;
   Error::ErrorCode ret = Error::NO_ERROR_LBF;
   for (const auto& kv : m_floodfile->m_files) {
@@ -119,7 +123,7 @@ Error::ErrorCode Flood::ReadVerifiedChunk(const std::string& i_filename, U32 i_c
     o_data.clear();
     return Error::NO_ERROR_LBF;
   }
-  lbf_ctx* ctx = Encoder::Context();
+  lbf_ctx* ctx = Ctx();
   if (!ctx) return Error::UNKNOWN_ERROR_LBF;
   const U64 zero = 0;
   const U32 sz = chunk.m_size;
@@ -147,7 +151,7 @@ Error::ErrorCode Flood::ReceiveChunk(const std::string& i_filename, U32 i_chunki
   if (chunk.m_size != i_size) return Error::NO_ERROR_LBF;  // :156
   U8 expected[20];
   if (!decode_hash(chunk.m_hash, expected)) return Error::NO_ERROR_LBF;
-  lbf_ctx* ctx = Encoder::Context();
+  lbf_ctx* ctx = Ctx();
   if (!ctx) return Error::UNKNOWN_ERROR_LBF;
   const U64 zero = 0;
   U8 verdict = 0;
@@ -167,6 +171,124 @@ Error::ErrorCode Flood::ReceiveChunk(const std::string& i_filename, U32 i_chunki
   rtf.m_chunkmap[i_chunkindex] = '1';  // :181-185
   m_chunkstodownload.erase(P_ChunkKey(it->first, i_chunkindex));
   o_accepted = true;
+  return Error::NO_ERROR_LBF;
+}
+
+Error::ErrorCode Flood::ReadVerifiedChunks(const std::vector<P_ChunkKey>& i_keys, V_U8& o_arena, V_U64& o_offsets,
+                                           std::string& o_valid) {
+  const size_t n = i_keys.size();
+  o_offsets.assign(n, 0);
+  o_valid.assign(n, '0');
+  V_U32 sizes(n, 0);
+  V_U8 expected(n * 20, 0);
+  std::vector<int> ok(n, 0);
+  U64 total = 0;
+  for (size_t k = 0; k < n; ++k) {
+    auto it = m_runtimefiles.find(i_keys[k].first);
+    if (it == m_runtimefiles.end() || i_keys[k].second >= it->second.m_file->m_chunks.size()) continue;
+    const FloodFile::Chunk& c = it->second.m_file->m_chunks[i_keys[k].second];
+    if (!decode_hash(c.m_hash, &expected[20 * k])) continue;
+    o_offsets[k] = total;
+    sizes[k] = c.m_size;
+    total += (c.m_size + 15) & ~15ull;  // keep every chunk 16-byte aligned in the arena
+    ok[k] = 1;
+  }
+  o_arena.assign(total ? total : 1, 0);
+  // one open per file, pread per chunk (ChunkMethods.cpp:105-115 fopen/fread per request)
+  std::map<std::string, int> fds;
+  for (size_t k = 0; k < n; ++k) {
+    if (!ok[k]) continue;
+    const std::string& name = i_keys[k].first;
+    auto f = fds.find(name);
+    if (f == fds.end()) f = fds.emplace(name, open(PathOf(name).c_str(), O_RDONLY)).first;
+    const RuntimeFile& rtf = m_runtimefiles[name];
+    const off_t off = (off_t)rtf.m_chunkoffsets[i_keys[k].second];
+    U64 got = 0;
+    while (f->second >= 0 && got < sizes[k]) {
+      const ssize_t r = pread(f->second, &o_arena[o_offsets[k]] + got, sizes[k] - got, off + (off_t)got);
+      if (r <= 0) break;
+      got += (U64)r;
+    }
+    if (got != sizes[k]) ok[k] = 0;
+  }
+  for (auto& f : fds)
+    if (f.second >= 0) close(f.second);
+  std::vector<U64> voff;
+  std::vector<U32> vsz;
+  std::vector<U8> vexp;
+  std::vector<size_t> which;
+  for (size_t k = 0; k < n; ++k) {
+    if (!ok[k]) continue;
+    which.push_back(k);
+    voff.push_back(o_offsets[k]);
+    vsz.push_back(sizes[k]);
+    vexp.insert(vexp.end(), &expected[20 * k], &expected[20 * k] + 20);
+  }
+  if (which.empty()) return Error::NO_ERROR_LBF;
+  lbf_ctx* ctx = Ctx();
+  if (!ctx) return Error::UNKNOWN_ERROR_LBF;
+  std::vector<U8> verdict(which.size(), 0);
+  if (lbf_verify_batch(ctx, &o_arena[0], o_arena.size(), &voff[0], &vsz[0], which.size(), &vexp[0], &verdict[0],
+                       LBF_HOST_PTR) != LBF_OK)
+    return Error::UNKNOWN_ERROR_LBF;
+  for (size_t j = 0; j < which.size(); ++j)
+    if (verdict[j]) o_valid[which[j]] = '1';
+  return Error::NO_ERROR_LBF;
+}
+
+Error::ErrorCode Flood::ReceiveChunks(const U8* i_arena, U64 i_arena_len, const std::vector<ChunkArrival>& i_chunks,
+                                      std::string& o_accepted) {
+  const size_t n = i_chunks.size();
+  o_accepted.assign(n, '0');
+  std::vector<U64> voff;
+  std::vector<U32> vsz;
+  std::vector<U8> vexp;
+  std::vector<size_t> which;
+  for (size_t k = 0; k < n; ++k) {
+    const ChunkArrival& a = i_chunks[k];
+    auto it = m_runtimefiles.find(a.m_filename);
+    if (it == m_runtimefiles.end() || a.m_index >= it->second.m_file->m_chunks.size()) continue;
+    const FloodFile::Chunk& c = it->second.m_file->m_chunks[a.m_index];
+    if (c.m_size != a.m_size) continue;  // ChunkMethods.cpp:156
+    if (a.m_offset > i_arena_len || a.m_size > i_arena_len - a.m_offset) continue;
+    U8 e[20];
+    if (!decode_hash(c.m_hash, e)) continue;
+    which.push_back(k);
+    voff.push_back(a.m_offset);
+    vsz.push_back(a.m_size);
+    vexp.insert(vexp.end(), e, e + 20);
+  }
+  if (which.empty()) return Error::NO_ERROR_LBF;
+  lbf_ctx* ctx = Ctx();
+  if (!ctx) return Error::UNKNOWN_ERROR_LBF;
+  std::vector<U8> verdict(which.size(), 0);
+  static const U8 kEmpty = 0;
+  if (lbf_verify_batch(ctx, i_arena_len ? i_arena : &kEmpty, i_arena_len, &voff[0], &vsz[0], which.size(), &vexp[0],
+                       &verdict[0], LBF_HOST_PTR) != LBF_OK)
+    return Error::UNKNOWN_ERROR_LBF;
+  // write the accepted chunks: one open per file (fopen "r+b" else "w+b", :169-173)
+  std::map<std::string, int> fds;
+  for (size_t j = 0; j < which.size(); ++j) {
+    if (!verdict[j]) continue;  // bad chunk silently dropped (:167)
+    const ChunkArrival& a = i_chunks[which[j]];
+    auto f = fds.find(a.m_filename);
+    if (f == fds.end()) f = fds.emplace(a.m_filename, open(PathOf(a.m_filename).c_str(), O_RDWR | O_CREAT, 0644)).first;
+    if (f->second < 0) continue;
+    RuntimeFile& rtf = m_runtimefiles[a.m_filename];
+    const off_t off = (off_t)rtf.m_chunkoffsets[a.m_index];
+    U64 put = 0;
+    while (put < a.m_size) {
+      const ssize_t w = pwrite(f->second, i_arena + a.m_offset + put, a.m_size - put, off + (off_t)put);
+      if (w <= 0) break;
+      put += (U64)w;
+    }
+    if (put != a.m_size) continue;
+    rtf.m_chunkmap[a.m_index] = '1';  // :181-185
+    m_chunkstodownload.erase(P_ChunkKey(a.m_filename, a.m_index));
+    o_accepted[which[j]] = '1';
+  }
+  for (auto& f : fds)
+    if (f.second >= 0) close(f.second);
   return Error::NO_ERROR_LBF;
 }
 

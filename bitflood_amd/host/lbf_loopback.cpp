@@ -1,0 +1,503 @@
+// lbf_loopback.cpp -- configuration C5: two peers over loopback TCP, every
+// received chunk verified on the GPU before it is written.
+//
+// Seeder  : a test_client that holds the whole file.  For RequestChunk it reads
+//           the chunk, re-verifies it and answers SendChunk only if it matches
+//           (ChunkMethodHandler::_HandleRequestChunk, ChunkMethods.cpp:89-135).
+// Leecher : a test_client that holds nothing.  It asks for chunks
+//           (Flood::LoopOnce, Flood.cpp:85-165) and handles SendChunk by size
+//           check, verify, write at the chunk's offset, chunkmap '1'
+//           (_HandleSendChunk, ChunkMethods.cpp:137-225).
+// Both speak the reference's frames (include/libBitFlood/PeerWire.H).
+//
+// What differs from the reference loop, on purpose:
+//  - no tracker: the leecher connects to the seeder directly (registration is
+//    control plane, out of scope);
+//  - no pacing: the reference sleeps 100 ms per loop and asks for one chunk per
+//    loop (test_client.cpp:72-76, Flood.cpp:95-141), about 10 chunks/s.  Here the
+//    leecher keeps --window requests outstanding;
+//  - batched verify: up to --batch arrivals per GPU launch (Flood::ReceiveChunks)
+//    and up to --batch requests per launch on the seeder (ReadVerifiedChunks).
+// With --corrupt K the seeder flips one byte of every K-th chunk AFTER its own
+// verify (a wire error); the leecher must reject it and ask again.
+//
+// Prints one JSON line: payload rate, verify latency, batch sizes, and the end
+// state (resume verify of the written file, byte comparison with the source).
+#include <arpa/inet.h>
+#include <fcntl.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <sys/socket.h>
+#include <sys/stat.h>
+#include <sys/statvfs.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "lbf_hash.h"
+#include "libBitFlood/Encoder.H"
+#include "libBitFlood/Flood.H"
+#include "libBitFlood/FloodFile.H"
+#include "libBitFlood/PeerWire.H"
+
+using namespace libBitFlood;
+using Clock = std::chrono::steady_clock;
+
+namespace {
+
+struct Opts {
+  U64 size = 256ull << 20;
+  U32 chunksize = 262144;
+  U32 window = 512;
+  U32 batch = 128;
+  unsigned threads = 8;
+  U32 corrupt = 0;
+  std::string dir;
+  bool keep = false;
+};
+
+[[noreturn]] void die(const std::string& m) {
+  fprintf(stderr, "lbf_loopback: %s\n", m.c_str());
+  exit(2);
+}
+
+double secs(Clock::time_point a, Clock::time_point b) { return std::chrono::duration<double>(b - a).count(); }
+
+template <class F>
+void parallel_for(size_t n, unsigned threads, F f) {
+  if (n <= 1 || threads <= 1) {
+    for (size_t k = 0; k < n; ++k) f(k);
+    return;
+  }
+  std::atomic<size_t> next{0};
+  std::vector<std::thread> th;
+  for (unsigned t = 0; t < std::min<size_t>(threads, n); ++t)
+    th.emplace_back([&] {
+      for (size_t k; (k = next++) < n;) f(k);
+    });
+  for (auto& t : th) t.join();
+}
+
+// ---- sockets ---------------------------------------------------------------
+void tune(int fd) {
+  int one = 1, buf = 8 << 20;
+  setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+  setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &buf, sizeof(buf));
+  setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &buf, sizeof(buf));
+}
+
+int listen_loopback(int& port) {
+  const int fd = socket(AF_INET, SOCK_STREAM, 0);
+  if (fd < 0) die("socket failed");
+  int one = 1;
+  setsockopt(fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+  sockaddr_in a{};
+  a.sin_family = AF_INET;
+  a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+  a.sin_port = 0;
+  if (bind(fd, (sockaddr*)&a, sizeof(a)) != 0 || listen(fd, 1) != 0) die("bind/listen on 127.0.0.1 failed");
+  socklen_t len = sizeof(a);
+  getsockname(fd, (sockaddr*)&a, &len);
+  port = ntohs(a.sin_port);
+  return fd;
+}
+
+int connect_loopback(int port) {
+  const int fd = socket(AF_INET, SOCK_STREAM, 0);
+  sockaddr_in a{};
+  a.sin_family = AF_INET;
+  a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+  a.sin_port = htons((uint16_t)port);
+  if (fd < 0 || connect(fd, (sockaddr*)&a, sizeof(a)) != 0) die("connect to 127.0.0.1 failed");
+  tune(fd);
+  return fd;
+}
+
+bool send_all(int fd, const std::string& s) {
+  size_t put = 0;
+  while (put < s.size()) {
+    const ssize_t w = send(fd, s.data() + put, s.size() - put, MSG_NOSIGNAL);
+    if (w <= 0) return false;
+    put += (size_t)w;
+  }
+  return true;
+}
+
+// '\n'-delimited frames (PeerConnection.cpp:213-237).
+struct FrameReader {
+  explicit FrameReader(int f) : fd(f) {}
+  int fd;
+  std::string buf;
+  size_t head = 0, scan = 0;
+  bool buffered() {
+    return memchr(buf.data() + scan, '\n', buf.size() - scan) != nullptr;
+  }
+  bool next(std::string& frame) {
+    for (;;) {
+      const char* nl = (const char*)memchr(buf.data() + scan, '\n', buf.size() - scan);
+      if (nl) {
+        const size_t end = (size_t)(nl - buf.data());
+        frame.assign(buf.data() + head, end - head);
+        head = scan = end + 1;
+        if (head > (64u << 20)) {  // compact
+          buf.erase(0, head);
+          head = scan = 0;
+        }
+        return true;
+      }
+      scan = buf.size();
+      const size_t old = buf.size();
+      buf.resize(old + (4 << 20));
+      const ssize_t r = recv(fd, &buf[old], 4 << 20, 0);
+      buf.resize(old + (r > 0 ? (size_t)r : 0));
+      if (r <= 0) return false;
+    }
+  }
+};
+
+// ---- synthetic source file -------------------------------------------------
+// Counter-mode splitmix64, the same stream as the device fill (sha1_device.hpp).
+U64 synth_word(U64 seed, U64 k) {
+  U64 z = seed * 0xD1B54A32D192ED03ull + (k + 1) * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+void write_source(const std::string& path, U64 size, unsigned threads) {
+  const int fd = open(path.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
+  if (fd < 0) die("cannot create " + path);
+  const U64 block = 64ull << 20;
+  const U64 nblk = (size + block - 1) / block;
+  std::atomic<bool> ok{true};
+  parallel_for(nblk, threads, [&](size_t b) {
+    const U64 off = b * block, len = std::min(block, size - off);
+    std::vector<U64> w((len + 7) / 8);
+    for (U64 k = 0; k < w.size(); ++k) w[k] = synth_word(0xC5, off / 8 + k);
+    if (pwrite(fd, w.data(), len, (off_t)off) != (ssize_t)len) ok = false;
+  });
+  close(fd);
+  if (!ok) die("writing " + path + " failed");
+}
+
+bool files_equal(const std::string& a, const std::string& b) {
+  FILE* fa = fopen(a.c_str(), "rb");
+  FILE* fb = fopen(b.c_str(), "rb");
+  bool eq = fa && fb;
+  std::vector<char> x(16 << 20), y(16 << 20);
+  while (eq) {
+    const size_t ra = fread(x.data(), 1, x.size(), fa), rb = fread(y.data(), 1, y.size(), fb);
+    if (ra != rb || memcmp(x.data(), y.data(), ra) != 0) eq = false;
+    if (ra < x.size()) break;
+  }
+  if (fa) fclose(fa);
+  if (fb) fclose(fb);
+  return eq;
+}
+
+// ---- seeder ------------------------------------------------------------------
+struct SeederStats {
+  U64 requests = 0, sent = 0, refused = 0, corrupted = 0;
+  double verify_s = 0, encode_s = 0;
+};
+
+void seeder_main(int lfd, FloodFileSPtr ff, std::string root, const Opts& o, SeederStats& st) {
+  const int fd = accept(lfd, nullptr, nullptr);
+  if (fd < 0) die("accept failed");
+  tune(fd);
+  // the seeder is its own peer: its own GPU context (streams, staging)
+  lbf_ctx* ctx = nullptr;
+  if (lbf_ctx_create(0, &ctx) != LBF_OK) die(std::string("seeder: lbf_ctx_create: ") + lbf_last_error());
+  Flood fl;
+  fl.m_rootdir = root;
+  fl.m_ctx = ctx;
+  if (fl.Initialize(ff) != Error::NO_ERROR_LBF) die("seeder: Initialize failed: " + std::string(Encoder::LastError()));
+  FrameReader rd(fd);
+  std::string f, method;
+  std::vector<PeerWire::Value> params;
+  std::vector<Flood::P_ChunkKey> keys;
+  Flood::S_ChunkKey corrupted;
+  for (;;) {
+    if (!rd.next(f)) break;
+    keys.clear();
+    do {
+      if (PeerWire::DecodeMethod(f, method, params) && method == PeerWire::kRequestChunk && params.size() == 2 &&
+          params[0].m_type == PeerWire::Value::STRING && params[1].m_type == PeerWire::Value::INT)
+        keys.emplace_back(params[0].m_str, (U32)params[1].m_int);
+    } while (keys.size() < o.batch && rd.buffered() && rd.next(f));
+    st.requests += keys.size();
+    V_U8 arena;
+    V_U64 offs;
+    std::string valid;
+    auto t0 = Clock::now();
+    if (fl.ReadVerifiedChunks(keys, arena, offs, valid) != Error::NO_ERROR_LBF)
+      die("seeder: verify failed: " + std::string(Encoder::LastError()));
+    auto t1 = Clock::now();
+    // sizes and the (first-send-only) corruption decision, serially
+    std::vector<U32> sizes(keys.size(), 0);
+    std::vector<char> flip(keys.size(), 0);
+    for (size_t k = 0; k < keys.size(); ++k) {
+      if (valid[k] != '1') continue;
+      sizes[k] = fl.m_runtimefiles.find(keys[k].first)->second.m_file->m_chunks[keys[k].second].m_size;
+      if (o.corrupt && sizes[k] && keys[k].second % o.corrupt == o.corrupt - 1 && corrupted.insert(keys[k]).second) {
+        flip[k] = 1;
+        ++st.corrupted;
+      }
+    }
+    std::vector<std::string> out(keys.size());
+    parallel_for(keys.size(), o.threads, [&](size_t k) {
+      if (valid[k] != '1') return;  // "send only if equal" (ChunkMethods.cpp:117-123)
+      const U8* data = &arena[offs[k]];
+      std::vector<U8> tmp;
+      if (flip[k]) {  // a wire error after the seeder's own verify
+        tmp.assign(data, data + sizes[k]);
+        tmp[sizes[k] / 2] ^= 0x01;
+        data = tmp.data();
+      }
+      out[k] = PeerWire::EncodeSendChunk(keys[k].first, keys[k].second, data, sizes[k]);
+    });
+    auto t2 = Clock::now();
+    st.verify_s += secs(t0, t1);
+    st.encode_s += secs(t1, t2);
+    for (size_t k = 0; k < keys.size(); ++k) {
+      if (out[k].empty()) {
+        ++st.refused;
+        continue;
+      }
+      if (!send_all(fd, out[k])) break;
+      ++st.sent;
+    }
+  }
+  close(fd);
+  lbf_ctx_destroy(ctx);
+}
+
+// ---- leecher -------------------------------------------------------------------
+struct Arrival {
+  std::string frame;
+  Clock::time_point t;
+};
+
+struct Queue {
+  std::mutex mu;
+  std::condition_variable cv;
+  std::deque<Arrival> q;
+  bool closed = false;
+};
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  Opts o;
+  for (int i = 1; i < argc; ++i) {
+    const std::string a = argv[i];
+    auto val = [&]() -> const char* {
+      if (i + 1 >= argc) die("missing value for " + a);
+      return argv[++i];
+    };
+    if (a == "--size") o.size = strtoull(val(), nullptr, 10);
+    else if (a == "--chunksize") o.chunksize = (U32)strtoul(val(), nullptr, 10);
+    else if (a == "--window") o.window = (U32)strtoul(val(), nullptr, 10);
+    else if (a == "--batch") o.batch = (U32)strtoul(val(), nullptr, 10);
+    else if (a == "--threads") o.threads = (unsigned)strtoul(val(), nullptr, 10);
+    else if (a == "--corrupt") o.corrupt = (U32)strtoul(val(), nullptr, 10);
+    else if (a == "--dir") o.dir = val();
+    else if (a == "--keep") o.keep = true;
+    else {
+      fprintf(stderr,
+              "usage: lbf_loopback [--size BYTES] [--chunksize N] [--window W] [--batch B] [--threads T]\n"
+              "                    [--corrupt K] [--dir DIR] [--keep]\n");
+      return 2;
+    }
+  }
+  if (o.chunksize == 0 || o.window == 0 || o.batch == 0) die("chunksize, window and batch must be > 0");
+  if (o.dir.empty()) {
+    const char* t = getenv("TMPDIR");
+    char tmpl[512];
+    snprintf(tmpl, sizeof(tmpl), "%s/lbf_loopback.XXXXXX", t && *t ? t : "/tmp");
+    if (!mkdtemp(tmpl)) die("mkdtemp failed");
+    o.dir = tmpl;
+  }
+  const std::string seeddir = o.dir + "/seed", leechdir = o.dir + "/leech";
+  mkdir(o.dir.c_str(), 0755);
+  mkdir(seeddir.c_str(), 0755);
+  mkdir(leechdir.c_str(), 0755);
+  struct statvfs vfs;
+  if (statvfs(o.dir.c_str(), &vfs) == 0 && (U64)vfs.f_bavail * vfs.f_frsize < 2 * o.size + (64 << 20))
+    die("not enough free space in " + o.dir + " for two copies of the file");
+
+  // The seeder's file and the flood file both peers load (test_encoder + test_client).
+  const std::string name = "c5.bin";
+  write_source(seeddir + "/" + name, o.size, o.threads);
+  Encoder::ToEncode te;
+  te.m_files.push_back(seeddir + "/" + name);
+  te.m_chunksize = o.chunksize;
+  FloodFile encoded;
+  auto te0 = Clock::now();
+  if (Encoder::EncodeFile(te, encoded) != Error::NO_ERROR_LBF) die("EncodeFile failed: " + std::string(Encoder::LastError()));
+  const double encode_s = secs(te0, Clock::now());
+  // peers address the file by its name relative to their own directory
+  FloodFileSPtr ff(new FloodFile());
+  for (auto& kv : encoded.m_files) {
+    FloodFile::FileSPtr file = kv.second;
+    file->m_name = name;
+    ff->m_files[name] = file;
+  }
+  const std::string floodpath = o.dir + "/c5.flood";
+  if (ff->ToXMLFile(floodpath) != Error::NO_ERROR_LBF) die("ToXMLFile failed");
+  FloodFileSPtr leech_ff(new FloodFile());
+  if (leech_ff->FromXMLFile(floodpath) != Error::NO_ERROR_LBF) die("FromXMLFile failed");
+
+  int port = 0;
+  const int lfd = listen_loopback(port);
+  SeederStats sst;
+  std::thread seeder(seeder_main, lfd, ff, seeddir, std::cref(o), std::ref(sst));
+
+  Flood fl;
+  fl.m_rootdir = leechdir;
+  if (fl.Initialize(leech_ff) != Error::NO_ERROR_LBF) die("leecher: Initialize failed: " + std::string(Encoder::LastError()));
+  std::deque<Flood::P_ChunkKey> todo(fl.m_chunkstodownload.begin(), fl.m_chunkstodownload.end());
+  const size_t total = todo.size();
+  const int fd = connect_loopback(port);
+
+  Queue q;
+  std::thread reader([&] {
+    FrameReader rd(fd);
+    std::string f;
+    while (rd.next(f)) {
+      const auto t = Clock::now();
+      std::lock_guard<std::mutex> g(q.mu);
+      q.q.push_back(Arrival{std::move(f), t});
+      q.cv.notify_one();
+    }
+    std::lock_guard<std::mutex> g(q.mu);
+    q.closed = true;
+    q.cv.notify_one();
+  });
+
+  const U64 slot = ((U64)o.chunksize + 15) & ~15ull;
+  V_U8 arena(slot * o.batch);
+  std::vector<double> lat_us;
+  lat_us.reserve(total);
+  size_t inflight = 0, accepted = 0, rejected = 0, batches = 0, wire_bytes = 0;
+  U64 payload = 0;
+  double decode_s = 0, verify_s = 0;
+  const auto t_start = Clock::now();
+  auto top_up = [&] {
+    std::string reqs;
+    while (inflight < o.window && !todo.empty()) {
+      const Flood::P_ChunkKey k = todo.front();
+      todo.pop_front();
+      reqs += PeerWire::EncodeMethod(PeerWire::kRequestChunk,
+                                     {PeerWire::Value::Str(k.first), PeerWire::Value::Int((int)k.second)});
+      ++inflight;
+    }
+    if (!reqs.empty() && !send_all(fd, reqs)) die("leecher: send failed");
+  };
+  top_up();
+  std::vector<Arrival> got;
+  while (accepted < total) {
+    got.clear();
+    {
+      std::unique_lock<std::mutex> g(q.mu);
+      if (!q.cv.wait_for(g, std::chrono::seconds(120), [&] { return !q.q.empty() || q.closed; }))
+        die("leecher: no chunk arrived for 120 s");
+      while (!q.q.empty() && got.size() < o.batch) {
+        got.push_back(std::move(q.q.front()));
+        q.q.pop_front();
+      }
+      if (got.empty() && q.closed) die("leecher: seeder closed the connection early");
+    }
+    // XmlRpcValue::binaryFromXml + the copy loop of :159-163, on `threads` cores
+    std::vector<Flood::ChunkArrival> arr(got.size());
+    std::vector<char> ok(got.size(), 0);
+    auto d0 = Clock::now();
+    parallel_for(got.size(), o.threads, [&](size_t k) {
+      size_t n = 0;
+      std::string fname;
+      U32 idx = 0;
+      if (PeerWire::DecodeSendChunk(got[k].frame.data(), got[k].frame.size(), fname, idx, &arena[k * slot],
+                                    o.chunksize, n)) {
+        arr[k] = Flood::ChunkArrival{fname, idx, k * slot, (U32)n};
+        ok[k] = 1;
+      }
+    });
+    auto d1 = Clock::now();
+    std::vector<Flood::ChunkArrival> batch;
+    std::vector<size_t> pos;
+    for (size_t k = 0; k < got.size(); ++k) {
+      wire_bytes += got[k].frame.size() + 1;
+      if (ok[k]) {
+        batch.push_back(arr[k]);
+        pos.push_back(k);
+      }
+    }
+    std::string acc;
+    if (fl.ReceiveChunks(arena.data(), arena.size(), batch, acc) != Error::NO_ERROR_LBF)
+      die("leecher: ReceiveChunks failed: " + std::string(Encoder::LastError()));
+    auto d2 = Clock::now();
+    decode_s += secs(d0, d1);
+    verify_s += secs(d1, d2);
+    ++batches;
+    inflight -= got.size();
+    for (size_t j = 0; j < batch.size(); ++j) {
+      lat_us.push_back(secs(got[pos[j]].t, d2) * 1e6);
+      if (acc[j] == '1') {
+        ++accepted;
+        payload += batch[j].m_size;
+      } else {
+        ++rejected;
+        todo.push_front(Flood::P_ChunkKey(batch[j].m_filename, batch[j].m_index));  // ask again
+      }
+    }
+    top_up();
+  }
+  const auto t_end = Clock::now();
+  shutdown(fd, SHUT_RDWR);
+  reader.join();
+  close(fd);
+  seeder.join();
+  close(lfd);
+
+  // end state: what a restarted leecher would find (Flood::_SetupFilesAndChunks)
+  Flood check;
+  check.m_rootdir = leechdir;
+  const bool resumed = check.Initialize(leech_ff) == Error::NO_ERROR_LBF && check.m_chunkstodownload.empty();
+  const bool same = files_equal(seeddir + "/" + name, leechdir + "/" + name);
+  std::sort(lat_us.begin(), lat_us.end());
+  auto pct = [&](double p) { return lat_us.empty() ? 0.0 : lat_us[std::min(lat_us.size() - 1, (size_t)(p * lat_us.size()))]; };
+  const double wall = secs(t_start, t_end);
+  printf("{\"config\": \"C5 loopback 2-peer\", \"bytes\": %llu, \"chunk_size\": %u, \"chunks\": %zu, "
+         "\"window\": %u, \"batch\": %u, \"threads\": %u, \"seconds\": %.3f, \"payload_gibs\": %.3f, "
+         "\"wire_gibs\": %.3f, \"encode_flood_s\": %.3f, "
+         "\"leecher\": {\"batches\": %zu, \"mean_batch\": %.1f, \"decode_s\": %.3f, \"verify_write_s\": %.3f, "
+         "\"rejected\": %zu}, \"seeder\": {\"requests\": %llu, \"sent\": %llu, \"refused\": %llu, \"verify_s\": %.3f, "
+         "\"encode_s\": %.3f}, \"verify_latency_us\": {\"p50\": %.0f, \"p90\": %.0f, \"p99\": %.0f, \"max\": %.0f}, "
+         "\"resume_verify_complete\": %s, \"files_identical\": %s, \"corrupt_every\": %u, \"corrupted_sent\": %llu}\n",
+         (unsigned long long)o.size, o.chunksize, total, o.window, o.batch, o.threads, wall,
+         payload / wall / (1u << 30), wire_bytes / wall / (1u << 30), encode_s, batches,
+         batches ? (double)(accepted + rejected) / batches : 0.0, decode_s, verify_s, rejected,
+         (unsigned long long)sst.requests, (unsigned long long)sst.sent, (unsigned long long)sst.refused, sst.verify_s,
+         sst.encode_s, pct(0.5), pct(0.9), pct(0.99), lat_us.empty() ? 0.0 : lat_us.back(), resumed ? "true" : "false",
+         same ? "true" : "false", o.corrupt, (unsigned long long)sst.corrupted);
+  if (!o.keep) {
+    unlink((seeddir + "/" + name).c_str());
+    unlink((leechdir + "/" + name).c_str());
+    unlink(floodpath.c_str());
+    rmdir(seeddir.c_str());
+    rmdir(leechdir.c_str());
+    rmdir(o.dir.c_str());
+  }
+  return resumed && same ? 0 : 1;
+}

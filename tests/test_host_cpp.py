@@ -7,6 +7,7 @@ for the DOMWriterImpl.cpp citations).  No reference run pins those bytes: the
 format is pinned by code reading.
 """
 import base64
+import json
 import hashlib
 import os
 import subprocess
@@ -56,6 +57,65 @@ def test_flood_file_format_unit():
     out = subprocess.run([os.path.join(LIB, "lbf_host_tests")], capture_output=True, text=True)
     assert out.returncode == 0, out.stderr
     assert "host_tests OK" in out.stdout
+
+
+def xmlrpc_base64(data: bytes) -> str:
+    """xmlrpc++ 0.7 base64 (base64.h:154-210) restated on Python's codec: a
+    newline after every 18th complete 4-char group, none after a padded one."""
+    s = base64.b64encode(data).decode()
+    full = len(data) // 3
+    out = []
+    for g in range(0, len(s) // 4):
+        out.append(s[4 * g:4 * g + 4])
+        if g < full and g % 18 == 17:
+            out.append("\n")
+    return "".join(out)
+
+
+def test_peer_wire_base64_vectors(tmp_path):
+    rng = np.random.default_rng(5)
+    lines = []
+    for n in [0, 1, 2, 3, 4, 53, 54, 55, 56, 107, 108, 109, 162, 1000, 4096, 65536]:
+        d = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        lines.append(f"{d.hex() or '-'} {xmlrpc_base64(d).replace(chr(10), chr(92) + 'n')}")
+    p = tmp_path / "vec.txt"
+    p.write_text("\n".join(lines) + "\n")
+    out = subprocess.run([os.path.join(LIB, "lbf_host_tests"), "--wire-vectors", str(p)],
+                         capture_output=True, text=True)
+    assert out.returncode == 0, out.stderr
+    assert f"wire_vectors OK {len(lines)}" in out.stdout
+
+
+@pytest.mark.skipif(_capi.device_count() > 0, reason="only meaningful without a GPU")
+def test_loopback_needs_gpu():
+    out = subprocess.run([os.path.join(LIB, "lbf_loopback"), "--size", "100000"], capture_output=True, text=True)
+    assert out.returncode == 2 and "no CPU fallback" in out.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("size,cs,window,batch,corrupt", [
+    (64 << 20, 262144, 64, 16, 0),                 # C5 chunk size, small file
+    ((16 << 20) + 12345, 65536, 512, 128, 7),      # odd tail, wire corruption every 7th chunk
+    (3 * 262144 + 1, 262144, 1, 1, 0),             # one chunk in flight, batch of one
+])
+def test_loopback_two_peers(tmp_path, size, cs, window, batch, corrupt):
+    """C5 shape: seeder and leecher over 127.0.0.1 speaking the reference's frames;
+    every arrival is GPU-verified before it is written; a corrupted arrival is
+    rejected and fetched again; the written file passes the resume verify and
+    equals the source byte for byte."""
+    out = subprocess.run([os.path.join(LIB, "lbf_loopback"), "--size", str(size), "--chunksize", str(cs),
+                          "--window", str(window), "--batch", str(batch), "--corrupt", str(corrupt),
+                          "--dir", str(tmp_path / "c5")], capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr + out.stdout
+    r = json.loads(out.stdout.strip().splitlines()[-1])
+    assert r["resume_verify_complete"] and r["files_identical"]
+    n = (size + cs - 1) // cs
+    assert r["chunks"] == n
+    if corrupt:
+        assert r["corrupted_sent"] == n // corrupt
+        assert r["leecher"]["rejected"] == r["corrupted_sent"]
+    else:
+        assert r["leecher"]["rejected"] == 0
 
 
 def test_expected_xml_helper_matches_cpp_unit_case():
