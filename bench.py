@@ -65,8 +65,15 @@ def dist_setup(args):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+        # one rank per GPU; more ranks than GPUs only for rehearsals of the
+        # multi-rank flow on a small box (LBF_BENCH_BACKEND=gloo)
+        dev = local % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(dev)
+        backend = os.environ.get("LBF_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(backend, rank=rank, world_size=world)
     else:
         torch.cuda.set_device(0)
     if args.gpus != world:

@@ -81,6 +81,7 @@ ORDERS = {
     "wk1/glb3": ("wk1", "SFPTQ", "", "split", "glb:3:128:use"),
     "wk1/glb3nouse": ("wk1", "SFPTQ", "", "split", "glb:3:128:nouse"),
     "wk1/mix3": ("wk1", "SFPTQ", "", "split", "mix:3:128:use"),
+    "wk1/mix3nouse": ("wk1", "SFPTQ", "", "split", "mix:3:128:nouse"),
     "wk1/half3": ("wk1", "SFPTQ", "", "split", "half:3:128:use"),
     "wk1/lds1": ("wk1", "SFPTQ", "", "split", "lds:1:128:use"),
     "wk1/lds3nouse": ("wk1", "SFPTQ", "", "split", "lds:3:128:nouse"),
@@ -157,8 +158,11 @@ def body(name):
             after = min(depth, 19 - q) * per   # reads issued after quad q's
             if src == "glb":
                 out.append(f"s_waitcnt vmcnt({after})")
-            elif src == "mix":
-                out.append("s_waitcnt vmcnt(0) lgkmcnt(0)" if True else "")
+            elif src in ("mix", "mix3b"):
+                # same-type reads issued after quad q's: odd quads go to VMEM
+                later = [r for r in range(q + 1, min(q + depth, 19) + 1)]
+                same = sum(1 for r in later if (r % 2) == (q % 2))
+                out.append(f"s_waitcnt vmcnt({same})" if q % 2 == 1 else f"s_waitcnt lgkmcnt({same})")
             else:
                 out.append(f"s_waitcnt lgkmcnt({after})")
         d = ops(i, style, bases)
