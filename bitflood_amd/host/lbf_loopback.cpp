@@ -212,6 +212,38 @@ struct SeederStats {
   double verify_s = 0, encode_s = 0;
 };
 
+// Blocking queue (closing wakes every waiter).
+template <class T>
+struct Chan {
+  std::mutex mu;
+  std::condition_variable cv;
+  std::deque<T> q;
+  bool closed = false;
+  void put(T v) {
+    std::lock_guard<std::mutex> g(mu);
+    q.push_back(std::move(v));
+    cv.notify_all();
+  }
+  void close() {
+    std::lock_guard<std::mutex> g(mu);
+    closed = true;
+    cv.notify_all();
+  }
+  // up to `max` items; blocks for the first; false once closed and drained
+  bool take(std::vector<T>& out, size_t max) {
+    out.clear();
+    std::unique_lock<std::mutex> g(mu);
+    cv.wait(g, [&] { return !q.empty() || closed; });
+    while (!q.empty() && out.size() < max) {
+      out.push_back(std::move(q.front()));
+      q.pop_front();
+    }
+    return !out.empty();
+  }
+};
+
+// Seeder pipeline: reader thread (frames -> request keys), this thread (read +
+// GPU verify + parallel encode of a batch), sender thread (frames -> socket).
 void seeder_main(int lfd, FloodFileSPtr ff, std::string root, const Opts& o, SeederStats& st) {
   const int fd = accept(lfd, nullptr, nullptr);
   if (fd < 0) die("accept failed");
@@ -223,19 +255,27 @@ void seeder_main(int lfd, FloodFileSPtr ff, std::string root, const Opts& o, See
   fl.m_rootdir = root;
   fl.m_ctx = ctx;
   if (fl.Initialize(ff) != Error::NO_ERROR_LBF) die("seeder: Initialize failed: " + std::string(Encoder::LastError()));
-  FrameReader rd(fd);
-  std::string f, method;
-  std::vector<PeerWire::Value> params;
-  std::vector<Flood::P_ChunkKey> keys;
-  Flood::S_ChunkKey corrupted;
-  for (;;) {
-    if (!rd.next(f)) break;
-    keys.clear();
-    do {
+  Chan<Flood::P_ChunkKey> requests;
+  Chan<std::string> outbox;
+  std::thread reader([&] {
+    FrameReader rd(fd);
+    std::string f, method;
+    std::vector<PeerWire::Value> params;
+    while (rd.next(f))
       if (PeerWire::DecodeMethod(f, method, params) && method == PeerWire::kRequestChunk && params.size() == 2 &&
           params[0].m_type == PeerWire::Value::STRING && params[1].m_type == PeerWire::Value::INT)
-        keys.emplace_back(params[0].m_str, (U32)params[1].m_int);
-    } while (keys.size() < o.batch && rd.buffered() && rd.next(f));
+        requests.put(Flood::P_ChunkKey(params[0].m_str, (U32)params[1].m_int));
+    requests.close();
+  });
+  std::thread sender([&] {
+    std::vector<std::string> msgs;
+    bool ok = true;
+    while (outbox.take(msgs, 64))
+      for (const std::string& m : msgs) ok = ok && send_all(fd, m);
+  });
+  std::vector<Flood::P_ChunkKey> keys;
+  Flood::S_ChunkKey corrupted;
+  while (requests.take(keys, o.batch)) {
     st.requests += keys.size();
     V_U8 arena;
     V_U64 offs;
@@ -270,15 +310,18 @@ void seeder_main(int lfd, FloodFileSPtr ff, std::string root, const Opts& o, See
     auto t2 = Clock::now();
     st.verify_s += secs(t0, t1);
     st.encode_s += secs(t1, t2);
-    for (size_t k = 0; k < keys.size(); ++k) {
-      if (out[k].empty()) {
+    for (std::string& m : out) {
+      if (m.empty()) {
         ++st.refused;
         continue;
       }
-      if (!send_all(fd, out[k])) break;
       ++st.sent;
+      outbox.put(std::move(m));
     }
   }
+  outbox.close();
+  sender.join();
+  reader.join();
   close(fd);
   lbf_ctx_destroy(ctx);
 }
@@ -289,12 +332,6 @@ struct Arrival {
   Clock::time_point t;
 };
 
-struct Queue {
-  std::mutex mu;
-  std::condition_variable cv;
-  std::deque<Arrival> q;
-  bool closed = false;
-};
 
 }  // namespace
 
@@ -368,33 +405,59 @@ int main(int argc, char** argv) {
   fl.m_rootdir = leechdir;
   if (fl.Initialize(leech_ff) != Error::NO_ERROR_LBF) die("leecher: Initialize failed: " + std::string(Encoder::LastError()));
   std::deque<Flood::P_ChunkKey> todo(fl.m_chunkstodownload.begin(), fl.m_chunkstodownload.end());
+  const std::vector<Flood::P_ChunkKey> all_keys(todo.begin(), todo.end());
   const size_t total = todo.size();
+  constexpr int kArenas = 3;
+  const U64 slot = ((U64)o.chunksize + 15) & ~15ull;
+  std::vector<V_U8> arenas(kArenas, V_U8(slot * o.batch));
   const int fd = connect_loopback(port);
 
-  Queue q;
+  // Leecher pipeline: reader thread (frames), this thread (decode into one of
+  // kArenas arenas, bookkeeping, requests), verifier thread (ReceiveChunks:
+  // GPU verify + write), so a batch's verify overlaps the next batch's decode.
+  struct Batch {
+    std::vector<Arrival> got;
+    std::vector<Flood::ChunkArrival> arr;
+    std::vector<size_t> pos;
+    int arena = 0;
+    std::string acc;
+    Clock::time_point done;
+    double verify_s = 0;
+  };
+  Chan<Arrival> arrivals;
+  Chan<Batch> to_verify, verified;
   std::thread reader([&] {
     FrameReader rd(fd);
     std::string f;
-    while (rd.next(f)) {
-      const auto t = Clock::now();
-      std::lock_guard<std::mutex> g(q.mu);
-      q.q.push_back(Arrival{std::move(f), t});
-      q.cv.notify_one();
+    while (rd.next(f)) arrivals.put(Arrival{std::move(f), Clock::now()});
+    arrivals.close();
+  });
+  std::thread verifier([&] {
+    std::vector<Batch> bs;
+    while (to_verify.take(bs, 1)) {
+      Batch& b = bs[0];
+      auto v0 = Clock::now();
+      if (fl.ReceiveChunks(arenas[b.arena].data(), arenas[b.arena].size(), b.arr, b.acc) != Error::NO_ERROR_LBF)
+        die("leecher: ReceiveChunks failed: " + std::string(Encoder::LastError()));
+      b.done = Clock::now();
+      b.verify_s = secs(v0, b.done);
+      verified.put(std::move(b));
     }
-    std::lock_guard<std::mutex> g(q.mu);
-    q.closed = true;
-    q.cv.notify_one();
   });
 
-  const U64 slot = ((U64)o.chunksize + 15) & ~15ull;
-  V_U8 arena(slot * o.batch);
   std::vector<double> lat_us;
   lat_us.reserve(total);
-  size_t inflight = 0, accepted = 0, rejected = 0, batches = 0, wire_bytes = 0;
+  size_t inflight = 0, accepted = 0, rejected = 0, batches = 0, wire_bytes = 0, undecodable = 0;
   U64 payload = 0;
   double decode_s = 0, verify_s = 0;
+  Flood::S_ChunkKey done;
+  std::vector<int> free_arenas;
+  for (int a = 0; a < kArenas; ++a) free_arenas.push_back(a);
   const auto t_start = Clock::now();
   auto top_up = [&] {
+    if (inflight == 0 && todo.empty() && done.size() < total)  // lost frames: ask again for what is missing
+      for (const auto& k : all_keys)
+        if (!done.count(k)) todo.push_back(k);
     std::string reqs;
     while (inflight < o.window && !todo.empty()) {
       const Flood::P_ChunkKey k = todo.front();
@@ -405,20 +468,73 @@ int main(int argc, char** argv) {
     }
     if (!reqs.empty() && !send_all(fd, reqs)) die("leecher: send failed");
   };
+  auto settle = [&](Batch& b) {
+    ++batches;
+    verify_s += b.verify_s;
+    inflight -= b.got.size();
+    for (size_t j = 0; j < b.arr.size(); ++j) {
+      lat_us.push_back(secs(b.got[b.pos[j]].t, b.done) * 1e6);
+      const Flood::P_ChunkKey key(b.arr[j].m_filename, b.arr[j].m_index);
+      if (b.acc[j] == '1') {
+        if (done.insert(key).second) {
+          ++accepted;
+          payload += b.arr[j].m_size;
+        }
+      } else {
+        ++rejected;
+        todo.push_front(key);  // ask again
+      }
+    }
+    free_arenas.push_back(b.arena);
+    top_up();
+  };
   top_up();
   std::vector<Arrival> got;
+  std::vector<Batch> res;
+  size_t in_verify = 0;
   while (accepted < total) {
+    // settle finished batches first (non-blocking), or wait for one when no arena is free
+    {
+      std::unique_lock<std::mutex> g(verified.mu);
+      if (free_arenas.empty())
+        if (!verified.cv.wait_for(g, std::chrono::seconds(120), [&] { return !verified.q.empty(); }))
+          die("leecher: verify stalled for 120 s");
+      res.clear();
+      while (!verified.q.empty()) {
+        res.push_back(std::move(verified.q.front()));
+        verified.q.pop_front();
+      }
+    }
+    for (Batch& b : res) {
+      --in_verify;
+      settle(b);
+    }
+    if (accepted >= total) break;
+    if (free_arenas.empty()) continue;
+    // next batch of arrivals (wait only if nothing is being verified)
     got.clear();
     {
-      std::unique_lock<std::mutex> g(q.mu);
-      if (!q.cv.wait_for(g, std::chrono::seconds(120), [&] { return !q.q.empty() || q.closed; }))
-        die("leecher: no chunk arrived for 120 s");
-      while (!q.q.empty() && got.size() < o.batch) {
-        got.push_back(std::move(q.q.front()));
-        q.q.pop_front();
+      std::unique_lock<std::mutex> g(arrivals.mu);
+      auto ready = [&] { return !arrivals.q.empty() || arrivals.closed; };
+      if (in_verify == 0) {
+        if (!arrivals.cv.wait_for(g, std::chrono::seconds(120), ready)) die("leecher: no chunk arrived for 120 s");
+      } else {
+        // a verify is running: start the next batch only once it is full, so
+        // batches grow to what arrives during one verify
+        auto full = [&] { return arrivals.q.size() >= o.batch || arrivals.closed; };
+        if (!arrivals.cv.wait_for(g, std::chrono::milliseconds(1), full)) continue;
       }
-      if (got.empty() && q.closed) die("leecher: seeder closed the connection early");
+      while (!arrivals.q.empty() && got.size() < o.batch) {
+        got.push_back(std::move(arrivals.q.front()));
+        arrivals.q.pop_front();
+      }
+      if (got.empty() && arrivals.closed && in_verify == 0) die("leecher: seeder closed the connection early");
     }
+    if (got.empty()) continue;
+    Batch b;
+    b.arena = free_arenas.back();
+    free_arenas.pop_back();
+    U8* arena = arenas[b.arena].data();
     // XmlRpcValue::binaryFromXml + the copy loop of :159-163, on `threads` cores
     std::vector<Flood::ChunkArrival> arr(got.size());
     std::vector<char> ok(got.size(), 0);
@@ -427,43 +543,30 @@ int main(int argc, char** argv) {
       size_t n = 0;
       std::string fname;
       U32 idx = 0;
-      if (PeerWire::DecodeSendChunk(got[k].frame.data(), got[k].frame.size(), fname, idx, &arena[k * slot],
+      if (PeerWire::DecodeSendChunk(got[k].frame.data(), got[k].frame.size(), fname, idx, arena + k * slot,
                                     o.chunksize, n)) {
         arr[k] = Flood::ChunkArrival{fname, idx, k * slot, (U32)n};
         ok[k] = 1;
       }
     });
-    auto d1 = Clock::now();
-    std::vector<Flood::ChunkArrival> batch;
-    std::vector<size_t> pos;
+    decode_s += secs(d0, Clock::now());
     for (size_t k = 0; k < got.size(); ++k) {
       wire_bytes += got[k].frame.size() + 1;
       if (ok[k]) {
-        batch.push_back(arr[k]);
-        pos.push_back(k);
-      }
-    }
-    std::string acc;
-    if (fl.ReceiveChunks(arena.data(), arena.size(), batch, acc) != Error::NO_ERROR_LBF)
-      die("leecher: ReceiveChunks failed: " + std::string(Encoder::LastError()));
-    auto d2 = Clock::now();
-    decode_s += secs(d0, d1);
-    verify_s += secs(d1, d2);
-    ++batches;
-    inflight -= got.size();
-    for (size_t j = 0; j < batch.size(); ++j) {
-      lat_us.push_back(secs(got[pos[j]].t, d2) * 1e6);
-      if (acc[j] == '1') {
-        ++accepted;
-        payload += batch[j].m_size;
+        b.arr.push_back(arr[k]);
+        b.pos.push_back(k);
       } else {
-        ++rejected;
-        todo.push_front(Flood::P_ChunkKey(batch[j].m_filename, batch[j].m_index));  // ask again
+        ++undecodable;
       }
     }
-    top_up();
+    b.got = std::move(got);
+    got = std::vector<Arrival>();
+    ++in_verify;
+    to_verify.put(std::move(b));
   }
   const auto t_end = Clock::now();
+  to_verify.close();
+  verifier.join();
   shutdown(fd, SHUT_RDWR);
   reader.join();
   close(fd);
@@ -482,12 +585,12 @@ int main(int argc, char** argv) {
          "\"window\": %u, \"batch\": %u, \"threads\": %u, \"seconds\": %.3f, \"payload_gibs\": %.3f, "
          "\"wire_gibs\": %.3f, \"encode_flood_s\": %.3f, "
          "\"leecher\": {\"batches\": %zu, \"mean_batch\": %.1f, \"decode_s\": %.3f, \"verify_write_s\": %.3f, "
-         "\"rejected\": %zu}, \"seeder\": {\"requests\": %llu, \"sent\": %llu, \"refused\": %llu, \"verify_s\": %.3f, "
+         "\"rejected\": %zu, \"undecodable\": %zu}, \"seeder\": {\"requests\": %llu, \"sent\": %llu, \"refused\": %llu, \"verify_s\": %.3f, "
          "\"encode_s\": %.3f}, \"verify_latency_us\": {\"p50\": %.0f, \"p90\": %.0f, \"p99\": %.0f, \"max\": %.0f}, "
          "\"resume_verify_complete\": %s, \"files_identical\": %s, \"corrupt_every\": %u, \"corrupted_sent\": %llu}\n",
          (unsigned long long)o.size, o.chunksize, total, o.window, o.batch, o.threads, wall,
          payload / wall / (1u << 30), wire_bytes / wall / (1u << 30), encode_s, batches,
-         batches ? (double)(accepted + rejected) / batches : 0.0, decode_s, verify_s, rejected,
+         batches ? (double)(accepted + rejected) / batches : 0.0, decode_s, verify_s, rejected, undecodable,
          (unsigned long long)sst.requests, (unsigned long long)sst.sent, (unsigned long long)sst.refused, sst.verify_s,
          sst.encode_s, pct(0.5), pct(0.9), pct(0.99), lat_us.empty() ? 0.0 : lat_us.back(), resumed ? "true" : "false",
          same ? "true" : "false", o.corrupt, (unsigned long long)sst.corrupted);
