@@ -13,6 +13,7 @@
 // Kernel "pc" (variant 2): producer/consumer split for few chains.
 // Kernel "lds" (variant 3): variant 1 with LDS-DMA staging, for many chains.
 // Kernel "pc2" (variant 4): one consumer + two producers, W+K hand-over, for few chains.
+// Kernel "pcx2" (variant 5): two pc pairs in one workgroup pinned to its CU, for 16-32 K chains.
 #include <hip/hip_runtime.h>
 
 #include <atomic>
@@ -245,16 +246,32 @@ __device__ __forceinline__ void pc_produce(uint4* ring, const ChainInfo& c, uint
 // (k+1) % 2 while the consumer computes step k from slot k % 2.  A 3-slot ring
 // that let the consumer prefetch step k+1 across the barrier measured 6 % slower
 // (extra VGPR traffic and LDS instructions inside the round chain).
-template <bool kUniform, int kRing>
-__global__ void __launch_bounds__(128) sha1_pc_kernel(ChunkParams p) {
-  extern __shared__ __attribute__((aligned(16))) uint4 ring[];  // W[kRing][20][64] | raw[4][4][64]
+// kPairs consumer/producer pairs per workgroup (waves 0..kPairs-1 consume,
+// kPairs..2*kPairs-1 produce; pair q = wave % kPairs).  kPairs = 2 with 112 KiB
+// of LDS pins ONE workgroup per CU, so each of its 4 waves has a SIMD to itself
+// -- for 16 K-32 K chains, where two 2- or 3-wave workgroups per CU would put
+// a consumer and a producer on one SIMD.
+template <bool kUniform, int kRing, int kPairs = 1>
+__global__ void __launch_bounds__(128 * kPairs) sha1_pc_kernel(ChunkParams p) {
+  extern __shared__ __attribute__((aligned(16))) uint4 lds_all[];  // per pair: W[kRing][20][64] | raw[4][4][64]
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const uint32_t i = blockIdx.x * kPcLanes + lane;
+  const int wave_id = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int pair = wave_id % kPairs;
+  const int wave = wave_id / kPairs;  // 0 = consumer, 1 = producer
+  uint4* ring = lds_all + pair * (pc_lds_bytes<kRing>() / 16);
+  const uint32_t i = blockIdx.x * (kPcLanes * kPairs) + pair * kPcLanes + lane;
   const ChainInfo c = chain_info<kUniform>(p, i);
-  // Identical in both waves; readfirstlane makes the loop bounds scalar so the
-  // barrier loops are uniform control flow.
-  const uint32_t nsteps = __builtin_amdgcn_readfirstlane(wave_max(c.total));
+  // Identical in every wave of the workgroup (every wave passes every
+  // barrier); readfirstlane keeps the loop bounds scalar.
+  uint32_t nsteps = __builtin_amdgcn_readfirstlane(wave_max(c.total));
+  if (kPairs > 1) {
+    __shared__ uint32_t wg_steps;
+    if (threadIdx.x == 0) wg_steps = 0;
+    __syncthreads();
+    if (lane == 0) atomicMax(&wg_steps, nsteps);
+    __syncthreads();
+    nsteps = __builtin_amdgcn_readfirstlane(wg_steps);
+  }
   const uint32_t nbarriers = nsteps;  // both waves pass exactly nsteps barriers
   constexpr uint32_t kAhead = kRing - 1;  // steps the producer runs ahead
 #ifdef LBF_PC_STAMPS
@@ -318,7 +335,7 @@ __global__ void __launch_bounds__(128) sha1_pc_kernel(ChunkParams p) {
   }
 #ifdef LBF_PC_STAMPS
   if (lane == 0) {
-    unsigned long long* o = g_pc_stamps + (blockIdx.x * 2 + wave) * 4;
+    unsigned long long* o = g_pc_stamps + (blockIdx.x * 2 * kPairs + wave_id) * 4;
     o[0] = acc[0];
     o[1] = acc[1];
     o[2] = acc[2];
@@ -556,8 +573,9 @@ __global__ void __launch_bounds__(256) fill_synth_kernel(uint8_t* dst, uint64_t 
 }
 
 std::atomic<int> g_variant{0};
-// Chain count up to which the pc kernel is chosen automatically (tuned on
-// MI355X, see DESIGN.md "kernel selection").
+// Chain counts up to which pc2 / pcx2 are chosen automatically (tuned on
+// MI355X, see DESIGN.md "kernel selection"): 64 chains per CU, 128 per CU.
+constexpr uint32_t kPc2MaxChains = 16384;
 constexpr uint32_t kPcMaxChains = 32768;
 
 }  // namespace
@@ -565,13 +583,14 @@ constexpr uint32_t kPcMaxChains = 32768;
 int pick_variant(uint64_t n) {
   int variant = g_variant.load();
   if (variant == 0) {
-    // Few chains: the per-chain instruction count bounds the time, so the
-    // schedule (with the round constants folded in) comes from two producer
-    // waves (4).  Many chains: every SIMD is busy and the fused one-chunk-per-lane
-    // kernel issues the fewest instructions in total; its LDS-staged form (3)
-    // measured equal or faster than the register form (1) at every point of
-    // tools/sweep_variants.py (profiles/r01/sweep_v123.log, sweep_v24.log).
-    variant = n <= kPcMaxChains ? 4 : 3;
+    // Few chains: the per-chain instruction count bounds the time.  Up to one
+    // 64-chain workgroup per CU, the schedule (round constants folded in) comes
+    // from two producer waves (4); up to two per CU, two plain consumer/producer
+    // pairs share one workgroup pinned to its CU so every wave owns a SIMD (5).
+    // Many chains: every SIMD is busy and the fused one-chunk-per-lane kernel
+    // issues the fewest instructions in total, LDS-staged (3).  Crossovers from
+    // tools/sweep_variants.py (profiles/r01/sweep_v123.log, sweep_v245.log).
+    variant = n <= kPc2MaxChains ? 4 : (n <= kPcMaxChains ? 5 : 3);
   }
   return variant;
 }
@@ -584,6 +603,18 @@ int launch_chunks(const ChunkParams& p, hipStream_t stream) {
     constexpr int lds = pc_lds_bytes<2>();
     if (p.offsets) hipLaunchKernelGGL((sha1_pc_kernel<false, 2>), dim3(blocks), dim3(128), lds, stream, p);
     else hipLaunchKernelGGL((sha1_pc_kernel<true, 2>), dim3(blocks), dim3(128), lds, stream, p);
+  } else if (variant == 5) {
+    constexpr int lds = 2 * pc_lds_bytes<2>();
+    static std::once_flag once;
+    std::call_once(once, [] {
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc_kernel<false, 2, 2>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc_kernel<true, 2, 2>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    });
+    const uint32_t blocks = (p.n + 2 * kPcLanes - 1) / (2 * kPcLanes);
+    if (p.offsets) hipLaunchKernelGGL((sha1_pc_kernel<false, 2, 2>), dim3(blocks), dim3(256), lds, stream, p);
+    else hipLaunchKernelGGL((sha1_pc_kernel<true, 2, 2>), dim3(blocks), dim3(256), lds, stream, p);
   } else if (variant == 4) {
     static std::once_flag once;
     std::call_once(once, [] {
@@ -671,7 +702,7 @@ extern "C" int lbf_sha1_uniform_launch(const uint8_t* d_base, uint64_t len, uint
 }
 
 extern "C" int lbf_set_kernel_variant(int variant) {
-  if (variant < 0 || variant > 4) return fail(LBF_ERR_INVALID, "unknown kernel variant");
+  if (variant < 0 || variant > 5) return fail(LBF_ERR_INVALID, "unknown kernel variant");
   lbf::g_variant.store(variant);
   return LBF_OK;
 }
