@@ -226,3 +226,21 @@ def test_cpp_api_gpu_suite(tmp_path):
     out = subprocess.run([os.path.join(LIB, "lbf_gpu_tests"), str(tmp_path)], capture_output=True, text=True)
     assert out.returncode == 0, out.stderr + out.stdout
     assert "gpu_tests OK" in out.stdout
+
+
+def test_wire_and_floodfile_parsers_fuzz_asan(tmp_path):
+    """Mutated peer frames and flood files through the parsers in an
+    ASAN/UBSan build of the host code (tools/fuzz_wire.cpp)."""
+    src = [os.path.join(ROOT, "tools", "fuzz_wire.cpp")] + [
+        os.path.join(ROOT, "bitflood_amd", "host", f) for f in ("PeerWire.cpp", "FloodFile.cpp", "Encoder.cpp", "Flood.cpp")]
+    exe = str(tmp_path / "fuzz_wire")
+    cc = subprocess.run(["g++", "-O1", "-g", "-std=c++17", "-fsanitize=address,undefined", "-fno-omit-frame-pointer",
+                         "-I" + os.path.join(ROOT, "include"), *src, "-L" + LIB, "-llbfhash", "-Wl,-rpath," + LIB,
+                         "-lpthread", "-o", exe], capture_output=True, text=True)
+    if cc.returncode != 0 and "sanitizer" in cc.stderr:
+        pytest.skip("no sanitizer runtime: " + cc.stderr[-200:])
+    assert cc.returncode == 0, cc.stderr
+    out = subprocess.run([exe, "20000"], capture_output=True, text=True, timeout=300,
+                         env={**os.environ, "UBSAN_OPTIONS": "halt_on_error=1", "ASAN_OPTIONS": "detect_leaks=0"})
+    assert out.returncode == 0, out.stderr[-3000:]
+    assert "fuzz_wire OK 20000" in out.stdout
