@@ -50,7 +50,9 @@ def main():
     if os.path.exists(stats):
         shutil.copy(stats, os.path.join(a.dst, "kernel_stats.csv"))
         for r in csv.DictReader(open(stats)):
-            if a.kernel in r["Name"]:
+            # rows are sorted by total time: keep the first match (the bench's
+            # device-resident kernel, not the host path's e2e launches)
+            if a.kernel in r["Name"] and "kernel" not in out:
                 out["kernel"] = r["Name"]
                 out["trace_avg_ns"] = float(r["AverageNs"])
                 out["trace_calls"] = int(r["Calls"])
