@@ -114,17 +114,47 @@ __device__ __forceinline__ void compress(Digest& s, uint32_t (&w)[16]) {
   s.h[4] += e;
 }
 
+// The four round constants in VGPRs.  A v_add3_u32 that reads K from an SGPR
+// costs a lone wave ≈5 more cycles per round than one reading three VGPRs
+// (25.6 vs 23.2 cycles per round, tools/probe_lds_lanes.hip modes 3/4), so the
+// consumers that add K themselves take it from here.  The asm keeps the
+// compiler from folding the constants back into SGPR operands.
+struct RoundK {
+  uint32_t k[4];
+  __device__ __forceinline__ RoundK() {
+    const uint32_t c[4] = {kK1, kK2, kK3, kK4};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) asm volatile("v_mov_b32 %0, %1" : "=v"(k[j]) : "s"(c[j]));
+  }
+};
+
+// One round of the two-add3 form with K from a VGPR:
+// t = rotl5(a) + f + (e + x + K).
+__device__ __forceinline__ void round_step_kv(int i, uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d,
+                                              uint32_t& e, uint32_t x, const RoundK& K) {
+  uint32_t f;
+  if (i < 20) f = f_choose(b, c, d);
+  else if (i < 40 || i >= 60) f = f_parity(b, c, d);
+  else f = f_major(b, c, d);
+  const uint32_t t = rotl(a, 5) + f + (e + x + K.k[i / 20]);
+  e = d;
+  d = c;
+  c = rotl(b, 30);
+  b = a;
+  a = t;
+}
+
 // Compression with the 80-word schedule already expanded (by a producer wave)
 // and stored in LDS as 20 uint4 per chain, `stride` uint4 apart.
-__device__ __forceinline__ void compress_expanded(Digest& s, const uint4* w, int stride) {
+__device__ __forceinline__ void compress_expanded(Digest& s, const uint4* w, int stride, const RoundK& K) {
   uint32_t a = s.h[0], b = s.h[1], c = s.h[2], d = s.h[3], e = s.h[4];
 #pragma unroll
   for (int q = 0; q < 20; ++q) {
     const uint4 v = w[q * stride];
-    round_step(4 * q + 0, a, b, c, d, e, v.x);
-    round_step(4 * q + 1, a, b, c, d, e, v.y);
-    round_step(4 * q + 2, a, b, c, d, e, v.z);
-    round_step(4 * q + 3, a, b, c, d, e, v.w);
+    round_step_kv(4 * q + 0, a, b, c, d, e, v.x, K);
+    round_step_kv(4 * q + 1, a, b, c, d, e, v.y, K);
+    round_step_kv(4 * q + 2, a, b, c, d, e, v.z, K);
+    round_step_kv(4 * q + 3, a, b, c, d, e, v.w, K);
   }
   s.h[0] += a;
   s.h[1] += b;

@@ -306,11 +306,12 @@ __global__ void __launch_bounds__(128 * kPairs) sha1_pc_kernel(ChunkParams p) {
     // ---------------- consumer ----------------
     Digest s;
     s.init();
+    const RoundK K;
     for (uint32_t k = 0; k < nsteps; ++k) {
       PC_STAMP(t0);
       __syncthreads();  // barrier k: slot k % 2 complete
       PC_STAMP(t1);
-      if (k < c.total) compress_expanded(s, ring + (k % kRing) * kPcSlotU4 + lane, kPcLanes);
+      if (k < c.total) compress_expanded(s, ring + (k % kRing) * kPcSlotU4 + lane, kPcLanes, K);
       PC_STAMP(t2);
       PC_ACC(0, t0, t1);
       PC_ACC(1, t1, t2);
