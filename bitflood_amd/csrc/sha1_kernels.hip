@@ -14,6 +14,7 @@
 // Kernel "lds" (variant 3): variant 1 with LDS-DMA staging, for many chains.
 // Kernel "pc2" (variant 4): one consumer + two producers, W+K hand-over, for few chains.
 // Kernel "pcx2" (variant 5): two pc pairs in one workgroup pinned to its CU, for 16-32 K chains.
+// Kernel "pc4" (variant 6): pc2 with the schedule double-buffered in registers, for <= 16 K chains.
 #include <hip/hip_runtime.h>
 
 #include <atomic>
@@ -196,6 +197,12 @@ __device__ __forceinline__ ChainInfo chain_info(const ChunkParams& p, uint32_t i
 __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, off, 64));
+  return v;
+}
+
+__device__ __forceinline__ uint32_t wave_min(uint32_t v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, off, 64));
   return v;
 }
 
@@ -477,6 +484,210 @@ __global__ void __launch_bounds__(192) sha1_pc2_kernel(ChunkParams p) {
 }
 
 // ---------------------------------------------------------------------------
+// Kernel "pc4" (variant 6): pc2 with the schedule double-buffered in the
+// consumer's registers.
+//
+// pc2's consumer loads step k's 80 words after barrier k and its first round
+// waits for the first of them: an LDS round trip per step, longer while the
+// producers' writes and DMA share the LDS.  Here the producers run one step
+// further ahead (step k+1 is complete at barrier k), and right after barrier k
+// the consumer loads ALL of step k+1 into a second register set while it runs
+// step k from the set it loaded one step earlier.  The loads complete during
+// the step, so no round ever waits for LDS.  Fifteen loads go out at once (the
+// lgkm counter holds 15) and five more after the fourth quad of rounds.  The
+// step loop is unrolled by two so the sets swap roles without copies.
+//
+// Interval b ends at barrier b.  In interval b producer (b+1) % 2 writes words
+// 40..79 of step b+1 and the other one words 0..39 of step b+2; interval 0
+// also builds steps 0 and 1 whole.  Step s is in slot s % 4: its first half
+// is written after barrier s-3, and the consumer finished loading step s-4
+// from that slot before barrier s-4 (3 slots would do; the fourth costs
+// nothing and makes the slot index a mask).  LDS 96 KiB: one
+// workgroup per CU, so each of the three waves has a SIMD of its own.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void write_result(const ChunkParams& p, uint32_t i, const Digest& s) {
+  uint32_t be[5];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) be[k] = bswap(s.h[k]);  // digest bytes in big-endian order
+  if (p.digests) {
+    uint32_t* o = reinterpret_cast<uint32_t*>(p.digests + 20ull * i);
+#pragma unroll
+    for (int k = 0; k < 5; ++k) o[k] = be[k];
+  }
+  if (p.verdicts) {
+    const uint32_t* e = reinterpret_cast<const uint32_t*>(p.expected + 20ull * i);
+    uint32_t diff = 0;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) diff |= be[k] ^ e[k];
+    p.verdicts[i] = diff == 0 ? 1 : 0;
+  }
+}
+
+constexpr int kPc4Ring = 4;
+constexpr int kPc4LdsBytes = (kPc4Ring * kPcSlotU4 + 2 * kP2Raw * kPcRawU4) * 16;
+constexpr int kPc4Early = 15;  // loads issued before the first round
+constexpr int kPc4LateAt = 3;  // the rest after quad 3's rounds
+
+// Step from `cur` (in registers); meanwhile the next step's 20 quads are
+// loaded from `next_slot` (this lane's column) into `nxt`.  Every lane runs
+// the rounds (no divergent branch around the late loads); a lane whose chain
+// has ended (`live` false) keeps its digest.
+__device__ __forceinline__ void pc4_compress(Digest& s, const uint4 (&cur)[kPcQuads], uint4 (&nxt)[kPcQuads],
+                                             const uint4* next_slot, bool live, bool all_live) {
+#pragma unroll
+  for (int q = 0; q < kPc4Early; ++q) nxt[q] = next_slot[q * kPcLanes];
+  // early loads go first (fenced on the digest, not on copies of it, so the
+  // working state needs no register copies)
+  asm volatile("" : "+v"(s.h[0]), "+v"(s.h[1]), "+v"(s.h[2]), "+v"(s.h[3]), "+v"(s.h[4])::"memory");
+  uint32_t a = s.h[0], b = s.h[1], c = s.h[2], d = s.h[3], e = s.h[4];
+#pragma unroll
+  for (int q = 0; q < kPcQuads; ++q) {
+    round_step_wk(4 * q + 0, a, b, c, d, e, cur[q].x);
+    round_step_wk(4 * q + 1, a, b, c, d, e, cur[q].y);
+    round_step_wk(4 * q + 2, a, b, c, d, e, cur[q].z);
+    round_step_wk(4 * q + 3, a, b, c, d, e, cur[q].w);
+    if (q == kPc4LateAt) {
+      // The two fences pin the late loads between quads 3 and 4: rounds are
+      // ordered through the state, loads through the memory clobber (left
+      // alone, the compiler sinks them to the end of the step, right before
+      // the barrier, which then waits for them).
+      asm volatile("" : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+v"(e)::"memory");
+#pragma unroll
+      for (int r = kPc4Early; r < kPcQuads; ++r) nxt[r] = next_slot[r * kPcLanes];
+      asm volatile("" : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+v"(e)::"memory");
+    }
+  }
+  if (all_live) {  // wave-uniform: every chain of the workgroup has this step
+    s.h[0] += a;
+    s.h[1] += b;
+    s.h[2] += c;
+    s.h[3] += d;
+    s.h[4] += e;
+  } else {
+    s.h[0] = live ? s.h[0] + a : s.h[0];
+    s.h[1] = live ? s.h[1] + b : s.h[1];
+    s.h[2] = live ? s.h[2] + c : s.h[2];
+    s.h[3] = live ? s.h[3] + d : s.h[3];
+    s.h[4] = live ? s.h[4] + e : s.h[4];
+  }
+}
+
+// A barrier the consumer's rounds cannot cross: the compiler may otherwise move
+// register-only round code over __syncthreads (it orders memory only), which
+// put a barrier right behind a fresh batch of loads and made it wait for them.
+#ifdef LBF_PC_STAMPS
+#define PC4_ACC_ARGS , unsigned long long (&acc)[4]
+#else
+#define PC4_ACC_ARGS
+#endif
+__device__ __forceinline__ void pc4_barrier(Digest& s PC4_ACC_ARGS) {
+  asm volatile("" : "+v"(s.h[0]), "+v"(s.h[1]), "+v"(s.h[2]), "+v"(s.h[3]), "+v"(s.h[4])::"memory");
+#ifdef LBF_PC_STAMPS
+  unsigned long long t0 = 0, t1 = 0;
+  PC_STAMP(t0);
+#endif
+  __syncthreads();
+#ifdef LBF_PC_STAMPS
+  PC_STAMP(t1);
+  PC_ACC(0, t0, t1);
+#endif
+  asm volatile("" : "+v"(s.h[0]), "+v"(s.h[1]), "+v"(s.h[2]), "+v"(s.h[3]), "+v"(s.h[4])::"memory");
+}
+
+template <bool kUniform>
+__global__ void __launch_bounds__(192) sha1_pc4_kernel(ChunkParams p) {
+  extern __shared__ __attribute__((aligned(16))) uint4 ring[];  // W[3][20][64] | raw[2][2][4][64]
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t i = blockIdx.x * kPcLanes + lane;
+  const ChainInfo c = chain_info<kUniform>(p, i);
+  const uint32_t nsteps = __builtin_amdgcn_readfirstlane(wave_max(c.total));
+#ifdef LBF_PC_STAMPS
+  unsigned long long acc[4] = {0, 0, 0, 0}, t0 = 0, t1 = 0, t2 = 0;
+#define PC4_ACC , acc
+#else
+#define PC4_ACC
+#endif
+
+  if (wave != 0) {
+    // ---------------- producer X = wave - 1: steps X, X+2, ... ----------------
+    const uint32_t X = wave - 1;
+    uint4* raw = ring + kPc4Ring * kPcSlotU4 + X * (kP2Raw * kPcRawU4);
+    const uint32_t raw_lds = (uint32_t)reinterpret_cast<uintptr_t>(raw);
+    p2_dma(c, X, raw_lds, 0);
+    p2_dma(c, X + 2, raw_lds, 1);
+    uint32_t w[16];
+    // words 0..39 of this producer's step `step` (its j-th); the raw slot is
+    // refilled with step + 4
+    auto first_half = [&](uint32_t step) {
+      const uint32_t j = (step - X) >> 1;
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // block j landed; only j+1's DMAs pending
+      p2_block(w, raw + (j & 1u) * kPcRawU4 + lane, c, step);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // raw slot read before it is refilled
+      p2_dma(c, step + 4, raw_lds, j & 1u);
+      expand_store_wk<0>(w, ring + (step % kPc4Ring) * kPcSlotU4 + lane, kPcLanes);
+    };
+    for (uint32_t b = 0; b < nsteps; ++b) {
+      PC_STAMP(t0);
+      if (b == 0 && X == 0) {  // prologue: step 0 whole
+        first_half(0);
+        expand_store_wk<1>(w, ring + lane, kPcLanes);
+      }
+      const uint32_t fin = b + 1;  // finished in interval b by producer fin % 2
+      if ((fin & 1u) == X && fin < nsteps) {
+        if (b == 0) first_half(fin);
+        expand_store_wk<1>(w, ring + (fin % kPc4Ring) * kPcSlotU4 + lane, kPcLanes);
+      }
+      const uint32_t start = b + 2;  // started in interval b by producer start % 2
+      if ((start & 1u) == X && start < nsteps) first_half(start);
+      PC_STAMP(t1);
+      __syncthreads();  // barrier b: steps <= b + 1 complete
+      PC_STAMP(t2);
+      PC_ACC(1, t0, t1);
+      PC_ACC(2, t1, t2);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA outlives the workgroup
+  } else {
+    // ---------------- consumer ----------------
+    Digest s;
+    s.init();
+    uint4 A[kPcQuads], B[kPcQuads];
+    // steps every chain of the workgroup has (inactive lanes count as having all)
+    const uint32_t min_steps =
+        __builtin_amdgcn_readfirstlane(wave_min(i < p.n ? c.total : 0xFFFFFFFFu));
+    if (nsteps > 0) {
+      __syncthreads();  // barrier 0: steps 0 and 1 complete
+#pragma unroll
+      for (int q = 0; q < kPcQuads; ++q) A[q] = ring[q * kPcLanes + lane];
+      // Once, so that the loop's first rounds need no wait on either path into
+      // it (otherwise every iteration waits for its own first load).
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+    }
+    for (uint32_t k = 0; k < nsteps; k += 2) {
+      // after barrier k: steps <= k+1 complete; A holds step k
+      pc4_compress(s, A, B, ring + ((k + 1) % kPc4Ring) * kPcSlotU4 + lane, k < c.total, k < min_steps);
+      if (k + 1 >= nsteps) break;
+      pc4_barrier(s PC4_ACC);  // barrier k+1
+      pc4_compress(s, B, A, ring + ((k + 2) % kPc4Ring) * kPcSlotU4 + lane, k + 1 < c.total,
+                   k + 1 < min_steps);
+      if (k + 2 >= nsteps) break;
+      pc4_barrier(s PC4_ACC);  // barrier k+2
+    }
+    if (i < p.n) write_result(p, i, s);
+  }
+#ifdef LBF_PC_STAMPS
+  if (lane == 0) {
+    unsigned long long* o = g_pc_stamps + (blockIdx.x * 3 + wave) * 4;
+    o[0] = acc[0];  // consumer: cycles at barriers
+    o[1] = acc[1];  // producer: work
+    o[2] = acc[2];  // producer: barrier
+    o[3] = nsteps;
+  }
+#endif
+#undef PC4_ACC
+}
+
+// ---------------------------------------------------------------------------
 // Kernel "lds" (variant 3): one chunk per lane for MANY chains.
 //
 // With >= 4 waves per SIMD the VALU itself is the limit (≈2,040 SIMD cycles per
@@ -574,9 +785,9 @@ __global__ void __launch_bounds__(256) fill_synth_kernel(uint8_t* dst, uint64_t 
 }
 
 std::atomic<int> g_variant{0};
-// Chain counts up to which pc2 / pcx2 are chosen automatically (tuned on
+// Chain counts up to which pc4 / pcx2 are chosen automatically (tuned on
 // MI355X, see DESIGN.md "kernel selection"): 64 chains per CU, 128 per CU.
-constexpr uint32_t kPc2MaxChains = 16384;
+constexpr uint32_t kPc4MaxChains = 16384;
 constexpr uint32_t kPcMaxChains = 32768;
 
 }  // namespace
@@ -586,12 +797,14 @@ int pick_variant(uint64_t n) {
   if (variant == 0) {
     // Few chains: the per-chain instruction count bounds the time.  Up to one
     // 64-chain workgroup per CU, the schedule (round constants folded in) comes
-    // from two producer waves (4); up to two per CU, two plain consumer/producer
-    // pairs share one workgroup pinned to its CU so every wave owns a SIMD (5).
-    // Many chains: every SIMD is busy and the fused one-chunk-per-lane kernel
-    // issues the fewest instructions in total, LDS-staged (3).  Crossovers from
-    // tools/sweep_variants.py (profiles/r01/sweep_v123.log, sweep_v245.log).
-    variant = n <= kPc2MaxChains ? 4 : (n <= kPcMaxChains ? 5 : 3);
+    // from two producer waves and is double-buffered in the consumer's
+    // registers (6); up to two per CU, two plain consumer/producer pairs share
+    // one workgroup pinned to its CU so every wave owns a SIMD (5).  Many
+    // chains: every SIMD is busy and the fused one-chunk-per-lane kernel issues
+    // the fewest instructions in total, LDS-staged (3).  Crossovers from
+    // tools/sweep_variants.py (profiles/r01/sweep_v123.log, sweep_v245.log,
+    // sweep_v46_pc4.log).
+    variant = n <= kPc4MaxChains ? 6 : (n <= kPcMaxChains ? 5 : 3);
   }
   return variant;
 }
@@ -627,6 +840,17 @@ int launch_chunks(const ChunkParams& p, hipStream_t stream) {
     const uint32_t blocks = (p.n + kPcLanes - 1) / kPcLanes;
     if (p.offsets) hipLaunchKernelGGL(sha1_pc2_kernel<false>, dim3(blocks), dim3(192), kP2LdsBytes, stream, p);
     else hipLaunchKernelGGL(sha1_pc2_kernel<true>, dim3(blocks), dim3(192), kP2LdsBytes, stream, p);
+  } else if (variant == 6) {
+    static std::once_flag once;
+    std::call_once(once, [] {
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4_kernel<false>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, kPc4LdsBytes);
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4_kernel<true>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, kPc4LdsBytes);
+    });
+    const uint32_t blocks = (p.n + kPcLanes - 1) / kPcLanes;
+    if (p.offsets) hipLaunchKernelGGL(sha1_pc4_kernel<false>, dim3(blocks), dim3(192), kPc4LdsBytes, stream, p);
+    else hipLaunchKernelGGL(sha1_pc4_kernel<true>, dim3(blocks), dim3(192), kPc4LdsBytes, stream, p);
   } else if (variant == 3) {
     const uint32_t blocks = (p.n + 255) / 256;
     constexpr int lds = 4 * kLdsStages * kPcRawU4 * 16;
@@ -703,7 +927,7 @@ extern "C" int lbf_sha1_uniform_launch(const uint8_t* d_base, uint64_t len, uint
 }
 
 extern "C" int lbf_set_kernel_variant(int variant) {
-  if (variant < 0 || variant > 5) return fail(LBF_ERR_INVALID, "unknown kernel variant");
+  if (variant < 0 || variant > 6) return fail(LBF_ERR_INVALID, "unknown kernel variant");
   lbf::g_variant.store(variant);
   return LBF_OK;
 }

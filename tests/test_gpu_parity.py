@@ -24,10 +24,10 @@ SEED_C = 0x5EED
 # 3 = one chunk per lane with LDS-DMA staging ("lds"), 4 = one consumer + two
 # producers with W+K hand-over ("pc2"), 5 = two consumer/producer pairs per
 # workgroup, one workgroup per CU ("pcx2")
-VARIANTS = [1, 2, 3, 4, 5]
+VARIANTS = [1, 2, 3, 4, 5, 6]
 
 
-@pytest.fixture(params=VARIANTS, ids=lambda v: {1: "lane", 2: "pc", 3: "lds", 4: "pc2", 5: "pcx2"}[v])
+@pytest.fixture(params=VARIANTS, ids=lambda v: {1: "lane", 2: "pc", 3: "lds", 4: "pc2", 5: "pcx2", 6: "pc4"}[v])
 def variant(request):
     H.set_kernel_variant(request.param)
     yield request.param

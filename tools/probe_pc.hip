@@ -19,7 +19,7 @@ static void run(int variant, uint8_t* buf, uint64_t len, uint32_t cs, uint8_t* d
     return;
   }
   const int wgs = (int)((n + 63) / 64);
-  const int nw = variant == 4 ? 3 : 2;  // waves per workgroup
+  const int nw = (variant == 4 || variant == 6) ? 3 : 2;  // waves per workgroup
   std::vector<unsigned long long> h(wgs * nw * 4);
   hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(lbf::g_pc_stamps), wgs * nw * 4 * 8, 0, hipMemcpyDeviceToHost);
   double a[3][3] = {{0}};
@@ -46,7 +46,7 @@ int main() {
   hipMalloc(&dig, (len / 65536) * 20);
   lbf_fill_synthetic(buf, len, 0x5EED, 0, nullptr);
   hipDeviceSynchronize();
-  for (int v : {2, 4}) {
+  for (int v : {4, 6}) {
     run(v, buf, len, 262144, dig);
     run(v, buf, len / 2, 262144, dig);
     run(v, buf, len, 1 << 20, dig);
