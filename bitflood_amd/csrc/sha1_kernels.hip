@@ -524,6 +524,19 @@ __device__ __forceinline__ void write_result(const ChunkParams& p, uint32_t i, c
 }
 
 constexpr int kPc4Ring = 4;
+// Diagnostic builds only (tools/probe_pc.hip): LBF_PC4_NOLOADS feeds the
+// rounds opaque registers instead of LDS words, LBF_PC4_NOBARRIER drops the
+// barriers.  Both give wrong digests; they isolate what loads and barriers cost.
+#ifdef LBF_PC4_NOLOADS
+#define PC4_LOAD(dst, src) asm volatile("" : "=v"((dst).x), "=v"((dst).y), "=v"((dst).z), "=v"((dst).w))
+#else
+#define PC4_LOAD(dst, src) (dst) = (src)
+#endif
+#ifdef LBF_PC4_NOBARRIER
+#define PC4_SYNC() do {} while (0)
+#else
+#define PC4_SYNC() __syncthreads()
+#endif
 constexpr int kPc4LdsBytes = (kPc4Ring * kPcSlotU4 + 2 * kP2Raw * kPcRawU4) * 16;
 constexpr int kPc4Early = 15;  // loads issued before the first round
 constexpr int kPc4LateAt = 3;  // the rest after quad 3's rounds
@@ -535,7 +548,7 @@ constexpr int kPc4LateAt = 3;  // the rest after quad 3's rounds
 __device__ __forceinline__ void pc4_compress(Digest& s, const uint4 (&cur)[kPcQuads], uint4 (&nxt)[kPcQuads],
                                              const uint4* next_slot, bool live, bool all_live) {
 #pragma unroll
-  for (int q = 0; q < kPc4Early; ++q) nxt[q] = next_slot[q * kPcLanes];
+  for (int q = 0; q < kPc4Early; ++q) PC4_LOAD(nxt[q], next_slot[q * kPcLanes]);
   // early loads go first (fenced on the digest, not on copies of it, so the
   // working state needs no register copies)
   asm volatile("" : "+v"(s.h[0]), "+v"(s.h[1]), "+v"(s.h[2]), "+v"(s.h[3]), "+v"(s.h[4])::"memory");
@@ -553,7 +566,7 @@ __device__ __forceinline__ void pc4_compress(Digest& s, const uint4 (&cur)[kPcQu
       // the barrier, which then waits for them).
       asm volatile("" : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+v"(e)::"memory");
 #pragma unroll
-      for (int r = kPc4Early; r < kPcQuads; ++r) nxt[r] = next_slot[r * kPcLanes];
+      for (int r = kPc4Early; r < kPcQuads; ++r) PC4_LOAD(nxt[r], next_slot[r * kPcLanes]);
       asm volatile("" : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+v"(e)::"memory");
     }
   }
@@ -586,7 +599,7 @@ __device__ __forceinline__ void pc4_barrier(Digest& s PC4_ACC_ARGS) {
   unsigned long long t0 = 0, t1 = 0;
   PC_STAMP(t0);
 #endif
-  __syncthreads();
+  PC4_SYNC();
 #ifdef LBF_PC_STAMPS
   PC_STAMP(t1);
   PC_ACC(0, t0, t1);
@@ -641,7 +654,7 @@ __global__ void __launch_bounds__(192) sha1_pc4_kernel(ChunkParams p) {
       const uint32_t start = b + 2;  // started in interval b by producer start % 2
       if ((start & 1u) == X && start < nsteps) first_half(start);
       PC_STAMP(t1);
-      __syncthreads();  // barrier b: steps <= b + 1 complete
+      PC4_SYNC();  // barrier b: steps <= b + 1 complete
       PC_STAMP(t2);
       PC_ACC(1, t0, t1);
       PC_ACC(2, t1, t2);
@@ -656,14 +669,28 @@ __global__ void __launch_bounds__(192) sha1_pc4_kernel(ChunkParams p) {
     const uint32_t min_steps =
         __builtin_amdgcn_readfirstlane(wave_min(i < p.n ? c.total : 0xFFFFFFFFu));
     if (nsteps > 0) {
-      __syncthreads();  // barrier 0: steps 0 and 1 complete
+      PC4_SYNC();  // barrier 0: steps 0 and 1 complete
 #pragma unroll
       for (int q = 0; q < kPcQuads; ++q) A[q] = ring[q * kPcLanes + lane];
       // Once, so that the loop's first rounds need no wait on either path into
       // it (otherwise every iteration waits for its own first load).
       __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
     }
-    for (uint32_t k = 0; k < nsteps; k += 2) {
+    uint32_t k = 0;
+    // Four steps per iteration while every chain of the workgroup is running
+    // and every step is followed by a barrier: k % 4 == 0, so the slots are
+    // compile-time offsets and the steps need no liveness checks.
+    for (; k + 4 <= min_steps && k + 4 < nsteps; k += 4) {
+      pc4_compress(s, A, B, ring + 1 * kPcSlotU4 + lane, true, true);
+      pc4_barrier(s PC4_ACC);  // barrier k+1
+      pc4_compress(s, B, A, ring + 2 * kPcSlotU4 + lane, true, true);
+      pc4_barrier(s PC4_ACC);  // barrier k+2
+      pc4_compress(s, A, B, ring + 3 * kPcSlotU4 + lane, true, true);
+      pc4_barrier(s PC4_ACC);  // barrier k+3
+      pc4_compress(s, B, A, ring + 0 * kPcSlotU4 + lane, true, true);
+      pc4_barrier(s PC4_ACC);  // barrier k+4
+    }
+    for (; k < nsteps; k += 2) {
       // after barrier k: steps <= k+1 complete; A holds step k
       pc4_compress(s, A, B, ring + ((k + 1) % kPc4Ring) * kPcSlotU4 + lane, k < c.total, k < min_steps);
       if (k + 1 >= nsteps) break;
