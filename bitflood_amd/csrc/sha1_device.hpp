@@ -246,6 +246,28 @@ __device__ __forceinline__ void expand_store_wk(uint32_t (&w)[16], uint4* out, i
   }
 }
 
+// expand_store_wk with the words stored as 20 uint2 pairs (`stride` uint2
+// apart) for consumers that read the schedule with ds_read_b64.
+template <int kHalf>
+__device__ __forceinline__ void expand_store_wk2(uint32_t (&w)[16], uint2* out, int stride) {
+#pragma unroll
+  for (int q = 20 * kHalf; q < 20 * kHalf + 20; ++q) {
+    uint32_t x[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int i = 2 * q + j;
+      if (i < 16) {
+        x[j] = w[i];
+      } else {
+        x[j] = sched(w[(i + 13) & 15], w[(i + 8) & 15], w[(i + 2) & 15], w[i & 15]);
+        w[i & 15] = x[j];
+      }
+      x[j] += round_k(i);
+    }
+    out[q * stride] = make_uint2(x[0], x[1]);
+  }
+}
+
 // Big-endian block from four 16-byte little-endian vectors.
 __device__ __forceinline__ void block_from_vec(uint32_t (&w)[16], const uint4& q0, const uint4& q1,
                                                const uint4& q2, const uint4& q3) {

@@ -15,6 +15,7 @@
 // Kernel "pc2" (variant 4): one consumer + two producers, W+K hand-over, for few chains.
 // Kernel "pcx2" (variant 5): two pc pairs in one workgroup pinned to its CU, for 16-32 K chains.
 // Kernel "pc4" (variant 6): pc2 with the schedule double-buffered in registers, for <= 16 K chains.
+// Kernel "pc4/b64" (variants 7, 8): pc4 with the schedule read as uint2 pairs (8: one ds_read_b64 each).
 #include <hip/hip_runtime.h>
 
 #include <atomic>
@@ -585,6 +586,102 @@ __device__ __forceinline__ void pc4_compress(Digest& s, const uint4 (&cur)[kPcQu
   }
 }
 
+// pc4_compress with the schedule read as 40 ds_read_b64 (variant 7).  A lone
+// wave pays ≈96 cycles per block for 20 ds_read_b128 over the same rounds fed
+// from registers, and ≈4 for 40 ds_read_b64 (tools/probe_lds_lanes.hip,
+// profiles/r01/probe_lds_lanes.log).  The lgkm counter holds 15, so the next
+// step's 40 pairs go out in three batches: before round 0, after round 16 and
+// after round 40, each pinned by fences like the late loads of pc4_compress.
+constexpr int kPc5Pairs = 40;
+constexpr int kPc5B1 = 15, kPc5B1At = 7;   // pairs 0..14 first; 15..27 after pair 7's rounds
+constexpr int kPc5B2 = 28, kPc5B2At = 19;  // pairs 28..39 after pair 19's rounds
+// kSplit keeps every load a single ds_read_b64: a memory fence between loads
+// stops the compiler from pairing them into ds_read2st64_b64 (which returns
+// four VGPRs per lane, like ds_read_b128).
+template <bool kSplit>
+__device__ __forceinline__ void pc5_load(uint2& dst, const uint2* base, int q) {
+  if (kSplit) asm volatile("" ::: "memory");  // the pairing pass does not look across it
+  dst = base[q * kPcLanes];
+}
+template <bool kSplit>
+__device__ __forceinline__ void pc5_compress(Digest& s, const uint2 (&cur)[kPc5Pairs], uint2 (&nxt)[kPc5Pairs],
+                                             const uint2* next_slot, bool live, bool all_live) {
+#pragma unroll
+  for (int q = 0; q < kPc5B1; ++q) pc5_load<kSplit>(nxt[q], next_slot, q);
+  asm volatile("" : "+v"(s.h[0]), "+v"(s.h[1]), "+v"(s.h[2]), "+v"(s.h[3]), "+v"(s.h[4])::"memory");
+  uint32_t a = s.h[0], b = s.h[1], c = s.h[2], d = s.h[3], e = s.h[4];
+#pragma unroll
+  for (int q = 0; q < kPc5Pairs; ++q) {
+    round_step_wk(2 * q + 0, a, b, c, d, e, cur[q].x);
+    round_step_wk(2 * q + 1, a, b, c, d, e, cur[q].y);
+    if (q == kPc5B1At || q == kPc5B2At) {
+      asm volatile("" : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+v"(e)::"memory");
+      const int lo = q == kPc5B1At ? kPc5B1 : kPc5B2;
+      const int hi = q == kPc5B1At ? kPc5B2 : kPc5Pairs;
+#pragma unroll
+      for (int r = lo; r < hi; ++r) pc5_load<kSplit>(nxt[r], next_slot, r);
+      asm volatile("" : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+v"(e)::"memory");
+    }
+  }
+  if (all_live) {
+    s.h[0] += a;
+    s.h[1] += b;
+    s.h[2] += c;
+    s.h[3] += d;
+    s.h[4] += e;
+  } else {
+    s.h[0] = live ? s.h[0] + a : s.h[0];
+    s.h[1] = live ? s.h[1] + b : s.h[1];
+    s.h[2] = live ? s.h[2] + c : s.h[2];
+    s.h[3] = live ? s.h[3] + d : s.h[3];
+    s.h[4] = live ? s.h[4] + e : s.h[4];
+  }
+}
+
+// The consumer's side of one pc4 step in either layout: uint4 quads (kVec 4,
+// variant 6) or uint2 pairs (kVec 2, variant 7) of the same 20 KiB slot.
+template <int kVec>
+struct Pc4Sched;
+template <>
+struct Pc4Sched<4> {
+  uint4 v[kPcQuads];
+  static __device__ __forceinline__ const uint4* col(const uint4* ring, int slot, int lane) {
+    return ring + slot * kPcSlotU4 + lane;
+  }
+  __device__ __forceinline__ void load_all(const uint4* src) {
+#pragma unroll
+    for (int q = 0; q < kPcQuads; ++q) v[q] = src[q * kPcLanes];
+  }
+};
+template <int kVec>
+struct Pc4Sched {  // kVec 2: uint2 pairs, loads may pair up; kVec 1: single ds_read_b64 each
+  uint2 v[kPc5Pairs];
+  static __device__ __forceinline__ const uint2* col(const uint4* ring, int slot, int lane) {
+    return reinterpret_cast<const uint2*>(ring + slot * kPcSlotU4) + lane;
+  }
+  __device__ __forceinline__ void load_all(const uint2* src) {
+#pragma unroll
+    for (int q = 0; q < kPc5Pairs; ++q) v[q] = src[q * kPcLanes];
+  }
+};
+__device__ __forceinline__ void pc4_step(Digest& s, const Pc4Sched<4>& cur, Pc4Sched<4>& nxt, const uint4* next_slot,
+                                         bool live, bool all_live) {
+  pc4_compress(s, cur.v, nxt.v, next_slot, live, all_live);
+}
+template <int kVec>
+__device__ __forceinline__ void pc4_step(Digest& s, const Pc4Sched<kVec>& cur, Pc4Sched<kVec>& nxt,
+                                         const uint2* next_slot, bool live, bool all_live) {
+  pc5_compress<kVec == 1>(s, cur.v, nxt.v, next_slot, live, all_live);
+}
+
+// Producer side: half kHalf of step `step` into its slot, in the kVec layout.
+template <int kVec, int kHalf>
+__device__ __forceinline__ void pc4_store_half(uint32_t (&w)[16], uint4* ring, uint32_t step, int lane) {
+  uint4* slot = ring + (step % 4) * kPcSlotU4;
+  if (kVec == 4) expand_store_wk<kHalf>(w, slot + lane, kPcLanes);
+  else expand_store_wk2<kHalf>(w, reinterpret_cast<uint2*>(slot) + lane, kPcLanes);
+}
+
 // A barrier the consumer's rounds cannot cross: the compiler may otherwise move
 // register-only round code over __syncthreads (it orders memory only), which
 // put a barrier right behind a fresh batch of loads and made it wait for them.
@@ -607,7 +704,7 @@ __device__ __forceinline__ void pc4_barrier(Digest& s PC4_ACC_ARGS) {
   asm volatile("" : "+v"(s.h[0]), "+v"(s.h[1]), "+v"(s.h[2]), "+v"(s.h[3]), "+v"(s.h[4])::"memory");
 }
 
-template <bool kUniform>
+template <bool kUniform, int kVec>
 __global__ void __launch_bounds__(192) sha1_pc4_kernel(ChunkParams p) {
   extern __shared__ __attribute__((aligned(16))) uint4 ring[];  // W[3][20][64] | raw[2][2][4][64]
   const int lane = threadIdx.x & 63;
@@ -638,18 +735,18 @@ __global__ void __launch_bounds__(192) sha1_pc4_kernel(ChunkParams p) {
       p2_block(w, raw + (j & 1u) * kPcRawU4 + lane, c, step);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // raw slot read before it is refilled
       p2_dma(c, step + 4, raw_lds, j & 1u);
-      expand_store_wk<0>(w, ring + (step % kPc4Ring) * kPcSlotU4 + lane, kPcLanes);
+      pc4_store_half<kVec, 0>(w, ring, step, lane);
     };
     for (uint32_t b = 0; b < nsteps; ++b) {
       PC_STAMP(t0);
       if (b == 0 && X == 0) {  // prologue: step 0 whole
         first_half(0);
-        expand_store_wk<1>(w, ring + lane, kPcLanes);
+        pc4_store_half<kVec, 1>(w, ring, 0, lane);
       }
       const uint32_t fin = b + 1;  // finished in interval b by producer fin % 2
       if ((fin & 1u) == X && fin < nsteps) {
         if (b == 0) first_half(fin);
-        expand_store_wk<1>(w, ring + (fin % kPc4Ring) * kPcSlotU4 + lane, kPcLanes);
+        pc4_store_half<kVec, 1>(w, ring, fin, lane);
       }
       const uint32_t start = b + 2;  // started in interval b by producer start % 2
       if ((start & 1u) == X && start < nsteps) first_half(start);
@@ -664,14 +761,13 @@ __global__ void __launch_bounds__(192) sha1_pc4_kernel(ChunkParams p) {
     // ---------------- consumer ----------------
     Digest s;
     s.init();
-    uint4 A[kPcQuads], B[kPcQuads];
+    Pc4Sched<kVec> A, B;
     // steps every chain of the workgroup has (inactive lanes count as having all)
     const uint32_t min_steps =
         __builtin_amdgcn_readfirstlane(wave_min(i < p.n ? c.total : 0xFFFFFFFFu));
     if (nsteps > 0) {
       PC4_SYNC();  // barrier 0: steps 0 and 1 complete
-#pragma unroll
-      for (int q = 0; q < kPcQuads; ++q) A[q] = ring[q * kPcLanes + lane];
+      A.load_all(Pc4Sched<kVec>::col(ring, 0, lane));
       // Once, so that the loop's first rounds need no wait on either path into
       // it (otherwise every iteration waits for its own first load).
       __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
@@ -681,22 +777,21 @@ __global__ void __launch_bounds__(192) sha1_pc4_kernel(ChunkParams p) {
     // and every step is followed by a barrier: k % 4 == 0, so the slots are
     // compile-time offsets and the steps need no liveness checks.
     for (; k + 4 <= min_steps && k + 4 < nsteps; k += 4) {
-      pc4_compress(s, A, B, ring + 1 * kPcSlotU4 + lane, true, true);
+      pc4_step(s, A, B, Pc4Sched<kVec>::col(ring, 1, lane), true, true);
       pc4_barrier(s PC4_ACC);  // barrier k+1
-      pc4_compress(s, B, A, ring + 2 * kPcSlotU4 + lane, true, true);
+      pc4_step(s, B, A, Pc4Sched<kVec>::col(ring, 2, lane), true, true);
       pc4_barrier(s PC4_ACC);  // barrier k+2
-      pc4_compress(s, A, B, ring + 3 * kPcSlotU4 + lane, true, true);
+      pc4_step(s, A, B, Pc4Sched<kVec>::col(ring, 3, lane), true, true);
       pc4_barrier(s PC4_ACC);  // barrier k+3
-      pc4_compress(s, B, A, ring + 0 * kPcSlotU4 + lane, true, true);
+      pc4_step(s, B, A, Pc4Sched<kVec>::col(ring, 0, lane), true, true);
       pc4_barrier(s PC4_ACC);  // barrier k+4
     }
     for (; k < nsteps; k += 2) {
       // after barrier k: steps <= k+1 complete; A holds step k
-      pc4_compress(s, A, B, ring + ((k + 1) % kPc4Ring) * kPcSlotU4 + lane, k < c.total, k < min_steps);
+      pc4_step(s, A, B, Pc4Sched<kVec>::col(ring, (k + 1) % kPc4Ring, lane), k < c.total, k < min_steps);
       if (k + 1 >= nsteps) break;
       pc4_barrier(s PC4_ACC);  // barrier k+1
-      pc4_compress(s, B, A, ring + ((k + 2) % kPc4Ring) * kPcSlotU4 + lane, k + 1 < c.total,
-                   k + 1 < min_steps);
+      pc4_step(s, B, A, Pc4Sched<kVec>::col(ring, (k + 2) % kPc4Ring, lane), k + 1 < c.total, k + 1 < min_steps);
       if (k + 2 >= nsteps) break;
       pc4_barrier(s PC4_ACC);  // barrier k+2
     }
@@ -825,13 +920,14 @@ int pick_variant(uint64_t n) {
     // Few chains: the per-chain instruction count bounds the time.  Up to one
     // 64-chain workgroup per CU, the schedule (round constants folded in) comes
     // from two producer waves and is double-buffered in the consumer's
-    // registers (6); up to two per CU, two plain consumer/producer pairs share
+    // registers, read as 8-byte pairs in three batches per step (7; 1-2 %
+    // ahead of the uint4 form 6, profiles/r01/sweep_v678.log); up to two per CU, two plain consumer/producer pairs share
     // one workgroup pinned to its CU so every wave owns a SIMD (5).  Many
     // chains: every SIMD is busy and the fused one-chunk-per-lane kernel issues
     // the fewest instructions in total, LDS-staged (3).  Crossovers from
     // tools/sweep_variants.py (profiles/r01/sweep_v123.log, sweep_v245.log,
     // sweep_v46_pc4.log).
-    variant = n <= kPc4MaxChains ? 6 : (n <= kPcMaxChains ? 5 : 3);
+    variant = n <= kPc4MaxChains ? 7 : (n <= kPcMaxChains ? 5 : 3);
   }
   return variant;
 }
@@ -867,17 +963,29 @@ int launch_chunks(const ChunkParams& p, hipStream_t stream) {
     const uint32_t blocks = (p.n + kPcLanes - 1) / kPcLanes;
     if (p.offsets) hipLaunchKernelGGL(sha1_pc2_kernel<false>, dim3(blocks), dim3(192), kP2LdsBytes, stream, p);
     else hipLaunchKernelGGL(sha1_pc2_kernel<true>, dim3(blocks), dim3(192), kP2LdsBytes, stream, p);
-  } else if (variant == 6) {
+  } else if (variant == 6 || variant == 7 || variant == 8) {
     static std::once_flag once;
     std::call_once(once, [] {
-      hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4_kernel<false>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, kPc4LdsBytes);
-      hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4_kernel<true>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, kPc4LdsBytes);
+      for (const void* f : {reinterpret_cast<const void*>(&sha1_pc4_kernel<false, 4>),
+                            reinterpret_cast<const void*>(&sha1_pc4_kernel<true, 4>),
+                            reinterpret_cast<const void*>(&sha1_pc4_kernel<false, 2>),
+                            reinterpret_cast<const void*>(&sha1_pc4_kernel<true, 2>),
+                            reinterpret_cast<const void*>(&sha1_pc4_kernel<false, 1>),
+                            reinterpret_cast<const void*>(&sha1_pc4_kernel<true, 1>)})
+        hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kPc4LdsBytes);
     });
     const uint32_t blocks = (p.n + kPcLanes - 1) / kPcLanes;
-    if (p.offsets) hipLaunchKernelGGL(sha1_pc4_kernel<false>, dim3(blocks), dim3(192), kPc4LdsBytes, stream, p);
-    else hipLaunchKernelGGL(sha1_pc4_kernel<true>, dim3(blocks), dim3(192), kPc4LdsBytes, stream, p);
+    const dim3 g(blocks), b(192);
+    if (variant == 6) {
+      if (p.offsets) hipLaunchKernelGGL((sha1_pc4_kernel<false, 4>), g, b, kPc4LdsBytes, stream, p);
+      else hipLaunchKernelGGL((sha1_pc4_kernel<true, 4>), g, b, kPc4LdsBytes, stream, p);
+    } else if (variant == 7) {
+      if (p.offsets) hipLaunchKernelGGL((sha1_pc4_kernel<false, 2>), g, b, kPc4LdsBytes, stream, p);
+      else hipLaunchKernelGGL((sha1_pc4_kernel<true, 2>), g, b, kPc4LdsBytes, stream, p);
+    } else {
+      if (p.offsets) hipLaunchKernelGGL((sha1_pc4_kernel<false, 1>), g, b, kPc4LdsBytes, stream, p);
+      else hipLaunchKernelGGL((sha1_pc4_kernel<true, 1>), g, b, kPc4LdsBytes, stream, p);
+    }
   } else if (variant == 3) {
     const uint32_t blocks = (p.n + 255) / 256;
     constexpr int lds = 4 * kLdsStages * kPcRawU4 * 16;
@@ -954,7 +1062,7 @@ extern "C" int lbf_sha1_uniform_launch(const uint8_t* d_base, uint64_t len, uint
 }
 
 extern "C" int lbf_set_kernel_variant(int variant) {
-  if (variant < 0 || variant > 6) return fail(LBF_ERR_INVALID, "unknown kernel variant");
+  if (variant < 0 || variant > 8) return fail(LBF_ERR_INVALID, "unknown kernel variant");
   lbf::g_variant.store(variant);
   return LBF_OK;
 }
