@@ -253,10 +253,13 @@ def main():
             "vs_baseline": None,
             "dtype": "u32",
             "data": "synthetic: counter-mode splitmix64 stream seed 0x5EED generated in HBM "
-                    "(rank r hashes bytes [r*4GiB,(r+1)*4GiB) of it)",
+                    f"(rank r hashes bytes [r*{file_bytes / GIB:g}GiB,(r+1)*{file_bytes / GIB:g}GiB) of it)",
             "config": {
                 "workload": "C2 per GPU: one 4 GiB file, 256 KiB chunks, SHA-1 -> 20 B digest per chunk "
-                            "(BASELINE.json configs[1]); N GPUs = N x 4 GiB file, contiguous chunk shards",
+                            "(BASELINE.json configs[1]); N GPUs = N x 4 GiB file, contiguous chunk shards"
+                            if (file_bytes, cs) == (4 * GIB, 262144) else
+                            f"custom per GPU: {file_bytes / GIB:g} GiB file, {cs // 1024} KiB chunks, SHA-1 -> 20 B "
+                            f"digest per chunk; N GPUs = N such shards (C4 per GPU is 32 GiB at 1024 KiB)",
                 "file_bytes_per_gpu": file_bytes,
                 "chunk_size": cs,
                 "chunks_per_gpu": n_chunks,
