@@ -39,7 +39,7 @@ N_SIMDS = 1024         # 256 CUs x 4 SIMDs
 KERNELS = {1: "sha1_lane_kernel<true>", 2: "sha1_pc_kernel<true, 2>", 3: "sha1_lds_kernel<true, 2>",
            4: "sha1_pc2_kernel<true>", 5: "sha1_pc_kernel<true, 2, 2>",
            6: "sha1_pc4_kernel<true, 4>", 7: "sha1_pc4_kernel<true, 2>", 8: "sha1_pc4_kernel<true, 1>",
-           9: "sha1_pcx4_kernel<true, 40>"}
+           9: "sha1_pcx4_kernel<true, 40>", 10: "sha1_pcx5_kernel<true, 64>"}
 # Issue floors per 64-byte block (tools/gen_round_order.py, tools/probe_lds_lanes.hip):
 #  pc2/pc4 consumer: 80 rounds x 5 VALU at one issue per 4.09 cycles -- the chain's own
 #    arithmetic alone (its 20 schedule loads and the barrier are not counted)
@@ -49,6 +49,8 @@ PC2_CYCLES_PER_BLOCK = 80 * 5 * 4.09
 PC_CYCLES_PER_BLOCK = 80 * 23.2
 #  pcx4 consumer: rounds 0..39 in the two-add3 form, 40..79 with W+K
 PCX4_CYCLES_PER_BLOCK = 40 * 23.2 + 40 * 5 * 4.09
+#  pcx5 consumer: rounds 0..63 in the two-add3 form, 64..79 with W+K, 16 byte swaps
+PCX5_CYCLES_PER_BLOCK = 64 * 23.2 + 16 * 5 * 4.09 + 16 * 4.09
 FUSED_VALU_PER_BLOCK = 613
 
 
@@ -170,6 +172,8 @@ def compute_floor_ms(variant, cs, n_chunks):
         return blocks * PC_CYCLES_PER_BLOCK / CLOCK_HZ * 1e3
     if variant == 9:
         return blocks * PCX4_CYCLES_PER_BLOCK / CLOCK_HZ * 1e3
+    if variant == 10:
+        return blocks * PCX5_CYCLES_PER_BLOCK / CLOCK_HZ * 1e3
     chain = blocks * FUSED_VALU_PER_BLOCK * 4.09 / CLOCK_HZ
     chip = n_chunks / 64 * blocks * FUSED_VALU_PER_BLOCK * 4.0 / (N_SIMDS * CLOCK_HZ)
     return max(chain, chip) * 1e3
@@ -279,7 +283,7 @@ def main():
             # SHA-1 is integer VALU work on a serial chain per chunk: the binding
             # limit is instruction issue, not HBM.
             "compute_floor": {
-                "bound": "per-chain issue" if variant in (2, 4, 5, 6, 7, 8, 9) else "valu",
+                "bound": "per-chain issue" if variant in (2, 4, 5, 6, 7, 8, 9, 10) else "valu",
                 "floor_ms": round(floor_ms, 4),
                 "frac": round(floor_ms / (launch_s * 1e3), 4),
                 "clock_ghz": CLOCK_HZ / 1e9,

@@ -291,6 +291,24 @@ __device__ __forceinline__ void expand_store_split(uint32_t (&w)[16], uint2* out
   }
 }
 
+// Words 16..79 of the schedule as 32 uint2 pairs (`stride` uint2 apart), K
+// added to words kKFrom..79: the consumer takes words 0..15 from the raw block.
+template <int kKFrom>
+__device__ __forceinline__ void expand_store_from16(uint32_t (&w)[16], uint2* out, int stride) {
+#pragma unroll
+  for (int q = 8; q < 40; ++q) {
+    uint32_t x[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int i = 2 * q + j;
+      x[j] = sched(w[(i + 13) & 15], w[(i + 8) & 15], w[(i + 2) & 15], w[i & 15]);
+      w[i & 15] = x[j];
+      if (i >= kKFrom) x[j] += round_k(i);
+    }
+    out[(q - 8) * stride] = make_uint2(x[0], x[1]);
+  }
+}
+
 // Big-endian block from four 16-byte little-endian vectors.
 __device__ __forceinline__ void block_from_vec(uint32_t (&w)[16], const uint4& q0, const uint4& q1,
                                                const uint4& q2, const uint4& q3) {
