@@ -230,13 +230,14 @@ int worker_init(Worker& w, int device) {
 void worker_free(Worker& w) {
   if (hipSetDevice(w.device) != hipSuccess) return;
   for (Slot& s : w.slot) {
-    if (s.stream) hipStreamSynchronize(s.stream);
-    hipFree(s.d_data); hipFree(s.d_off); hipFree(s.d_size);
-    hipFree(s.d_dig); hipFree(s.d_exp); hipFree(s.d_ver);
-    hipHostFree(s.h_data); hipHostFree(s.h_off); hipHostFree(s.h_size);
-    hipHostFree(s.h_dig); hipHostFree(s.h_exp); hipHostFree(s.h_ver);
+    // teardown: errors here have nowhere to go, the context is being destroyed
+    if (s.stream) (void)hipStreamSynchronize(s.stream);
+    for (void* d : {(void*)s.d_data, (void*)s.d_off, (void*)s.d_size, (void*)s.d_dig, (void*)s.d_exp, (void*)s.d_ver})
+      (void)hipFree(d);
+    for (void* h : {(void*)s.h_data, (void*)s.h_off, (void*)s.h_size, (void*)s.h_dig, (void*)s.h_exp, (void*)s.h_ver})
+      (void)hipHostFree(h);
     delete[] s.h_ok;
-    if (s.stream) hipStreamDestroy(s.stream);
+    if (s.stream) (void)hipStreamDestroy(s.stream);
     s = Slot{};
   }
 }

@@ -1499,19 +1499,23 @@ extern "C" int lbf_time_uniform(const uint8_t* d_base, uint64_t len, uint32_t ch
                                 float* out_ms_per_launch) {
   if (reps <= 0 || !out_ms_per_launch) return fail(LBF_ERR_INVALID, "lbf_time_uniform: bad reps/out");
   hipStream_t s = (hipStream_t)stream;
-  hipEvent_t e0, e1;
-  LBF_HIP_TRY(hipEventCreate(&e0));
-  LBF_HIP_TRY(hipEventCreate(&e1));
+  struct Events {  // destroyed on every return path
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    ~Events() {
+      if (e0) (void)hipEventDestroy(e0);
+      if (e1) (void)hipEventDestroy(e1);
+    }
+  } ev;
+  LBF_HIP_TRY(hipEventCreate(&ev.e0));
+  LBF_HIP_TRY(hipEventCreate(&ev.e1));
   int rc = LBF_OK;
-  LBF_HIP_TRY(hipEventRecord(e0, s));
+  LBF_HIP_TRY(hipEventRecord(ev.e0, s));
   for (int r = 0; r < reps && rc == LBF_OK; ++r)
     rc = lbf_sha1_uniform_launch(d_base, len, chunk_size, first_chunk, n, d_digests, nullptr, nullptr, stream);
-  LBF_HIP_TRY(hipEventRecord(e1, s));
-  LBF_HIP_TRY(hipEventSynchronize(e1));
+  LBF_HIP_TRY(hipEventRecord(ev.e1, s));
+  LBF_HIP_TRY(hipEventSynchronize(ev.e1));
   float ms = 0.f;
-  LBF_HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
-  hipEventDestroy(e0);
-  hipEventDestroy(e1);
+  LBF_HIP_TRY(hipEventElapsedTime(&ms, ev.e0, ev.e1));
   if (rc != LBF_OK) return rc;
   *out_ms_per_launch = ms / (float)reps;
   return LBF_OK;
