@@ -1192,7 +1192,8 @@ __global__ void __launch_bounds__(256) sha1_pcx5_kernel(ChunkParams p) {
 // K split for pcx5: the consumer adds K in rounds 0..63.  With the producer's
 // stores down to 16 KiB the two sides balance near there: splitting at 40 ran
 // 2 % slower, 48 and 56 within 0.5 % (profiles/r01/sweep_v9_pcx5_k40_k48.log,
-// sweep_pcx5_k48_k56_k64.log).
+// sweep_pcx5_k48_k56_k64.log); 72 ran 1.5 % and 80 (no K in the producer)
+// 5 % slower (sweep_pcx5_k64_k72_k80.log).
 constexpr int kPx5KFrom = 64;
 
 template <int kKFrom>
