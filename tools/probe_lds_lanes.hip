@@ -26,7 +26,8 @@ constexpr int kSlotU4 = 20 * 64;
 
 // mode 0: schedule from LDS (pc2 consumer); mode 1: from registers (floor);
 // mode 2: from LDS, two ds_read_b64 per 4 rounds; modes 3/4: two-add3 rounds from registers
-// with the round constant in an SGPR (3) or a VGPR (4)
+// with the round constant in an SGPR (3) or a VGPR (4); modes 5/6: the two-add3 round (5) and
+// the W+K round (6) from registers with rotl5(a) forced into the last add
 template <int kMode>
 __global__ void __launch_bounds__(64) consumer(uint32_t nblk, uint32_t lanes, uint32_t* out,
                                                unsigned long long* clk) {
@@ -52,6 +53,28 @@ __global__ void __launch_bounds__(64) consumer(uint32_t nblk, uint32_t lanes, ui
           round_step_wk(4 * q + 1, a, bb, c, d, e, r[q].y);
           round_step_wk(4 * q + 2, a, bb, c, d, e, r[q].z);
           round_step_wk(4 * q + 3, a, bb, c, d, e, r[q].w);
+        }
+        s.h[0] += a; s.h[1] += bb; s.h[2] += c; s.h[3] += d; s.h[4] += e;
+      } else if (kMode == 5 || kMode == 6) {
+        // the sum associated as written: the late operand rotl5(a) enters the
+        // LAST add (an empty asm keeps the compiler from reassociating);
+        // 5: t = add3(e, W, K) with K in VGPRs, 6: s = e + (W+K)
+        uint32_t kv[4] = {kK1, kK2, kK3, kK4};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) asm volatile("v_mov_b32 %0, %1" : "=v"(kv[j]) : "s"(kv[j]));
+        uint32_t a = s.h[0], bb = s.h[1], c = s.h[2], d = s.h[3], e = s.h[4];
+#pragma unroll
+        for (int q = 0; q < 20; ++q) {
+          const uint32_t x4[4] = {r[q].x, r[q].y, r[q].z, r[q].w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int i = 4 * q + j;
+            const uint32_t f = i < 20 ? f_choose(bb, c, d) : (i >= 40 && i < 60 ? f_major(bb, c, d) : f_parity(bb, c, d));
+            uint32_t t = kMode == 5 ? e + x4[j] + kv[i / 20] : e + x4[j];
+            asm("" : "+v"(t));
+            const uint32_t n = rotl(a, 5) + f + t;
+            e = d; d = c; c = rotl(bb, 30); bb = a; a = n;
+          }
         }
         s.h[0] += a; s.h[1] += bb; s.h[2] += c; s.h[3] += d; s.h[4] += e;
       } else if (kMode == 3 || kMode == 4) {
@@ -122,6 +145,8 @@ int main(int argc, char** argv) {
     run<1>("regs", nblk, lanes, out, clk);
     run<3>("2add3_sK", nblk, lanes, out, clk);
     run<4>("2add3_vK", nblk, lanes, out, clk);
+    run<5>("2add3_vK_late", nblk, lanes, out, clk);
+    run<6>("wk_late", nblk, lanes, out, clk);
   }
   return 0;
 }
