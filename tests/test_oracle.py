@@ -130,3 +130,34 @@ def test_c2_digest_of_digests(oracle, golden):
     assert hashlib.sha1(d.tobytes()).hexdigest() == c2["sha1_of_concat_raw_digests_hex"]
     for k, v in c2["samples_b64"].items():
         assert oracle.b64_27(bytes(d[int(k)])) == v
+
+
+from hypothesis import given, settings, strategies as st  # noqa: E402
+
+
+@settings(max_examples=200, deadline=None)
+@given(st.binary(min_size=0, max_size=1200))
+def test_sha1_property_vs_hashlib(oracle, data):
+    """Property: the restatement equals an independent SHA-1 (hashlib) on any bytes,
+    and its base64-27 string is hashlib's digest in unpadded standard base64."""
+    want = hashlib.sha1(data).digest()
+    assert oracle.sha1(data) == want
+    assert oracle.base64_encode(data) == base64.b64encode(want).decode().rstrip("=")
+
+
+@settings(max_examples=60, deadline=None)
+@given(st.lists(st.integers(min_value=0, max_value=700), min_size=1, max_size=24), st.integers(0, 2**31 - 1))
+def test_sha1_batch_property_ragged(oracle, sizes, seed):
+    """Property: the batch entry point over a ragged, overlapping-free chunk table at
+    arbitrary (unaligned) offsets equals hashlib chunk by chunk."""
+    rng = np.random.default_rng(seed)
+    gaps = rng.integers(0, 17, len(sizes))
+    offs, pos = [], 0
+    for g, s in zip(gaps, sizes):
+        pos += int(g)
+        offs.append(pos)
+        pos += s
+    base = rng.integers(0, 256, pos + 1, dtype=np.uint8)
+    got = oracle.sha1_batch(base, np.array(offs, np.uint64), np.array(sizes, np.uint32))
+    for k, (o, s) in enumerate(zip(offs, sizes)):
+        assert bytes(got[k]) == hashlib.sha1(base[o:o + s].tobytes()).digest()
