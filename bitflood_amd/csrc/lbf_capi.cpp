@@ -184,7 +184,8 @@ struct Slot {
 struct Worker {
   int device = 0;
   Slot slot[2];
-  uint64_t slot_bytes = 0;
+  uint64_t slot_bytes = 0;  // current staging capacity per slot (grown on demand)
+  uint64_t slot_max = 0;    // LBF_SLOT_MB: the largest a slot may grow
   uint64_t desc_cap = 0;
 };
 
@@ -203,20 +204,44 @@ uint64_t env_u64(const char* name, uint64_t dflt) {
   return strtoull(v, nullptr, 10);
 }
 
+// Staging memory is sized to the work, not reserved up front: pinning 2 x 512
+// MiB costs ≈200 ms at context creation and ≈110 ms at destruction
+// (tools/startup_probe.py), which a one-chunk Base64Encode or a small file
+// should not pay.  A slot grows, never shrinks, in 8 MiB steps up to slot_max.
+constexpr uint64_t kSlotStep = 8ull << 20;
+
+int ensure_slot_bytes(Worker& w, uint64_t need) {
+  need = std::min(w.slot_max, (std::max(need, kSlotStep) + kSlotStep - 1) / kSlotStep * kSlotStep);
+  if (need <= w.slot_bytes) return LBF_OK;
+  for (Slot& s : w.slot) {
+    LBF_HIP_TRY(hipStreamSynchronize(s.stream));
+    if (s.d_data) (void)hipFree(s.d_data);
+    if (s.h_data) (void)hipHostFree(s.h_data);
+    s.d_data = nullptr;
+    s.h_data = nullptr;
+  }
+  w.slot_bytes = 0;
+  for (Slot& s : w.slot) {
+    LBF_HIP_TRY(hipMalloc((void**)&s.d_data, need));
+    LBF_HIP_TRY(hipHostMalloc((void**)&s.h_data, need, hipHostMallocDefault));
+  }
+  w.slot_bytes = need;
+  return LBF_OK;
+}
+
 int worker_init(Worker& w, int device) {
   w.device = device;
-  w.slot_bytes = env_u64("LBF_SLOT_MB", 512) << 20;
+  w.slot_max = std::max<uint64_t>(env_u64("LBF_SLOT_MB", 512) << 20, 1ull << 20);
+  w.slot_bytes = 0;
   w.desc_cap = 1u << 16;
   LBF_HIP_TRY(hipSetDevice(device));
   for (Slot& s : w.slot) {
     LBF_HIP_TRY(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
-    LBF_HIP_TRY(hipMalloc((void**)&s.d_data, w.slot_bytes));
     LBF_HIP_TRY(hipMalloc((void**)&s.d_off, w.desc_cap * 8));
     LBF_HIP_TRY(hipMalloc((void**)&s.d_size, w.desc_cap * 4));
     LBF_HIP_TRY(hipMalloc((void**)&s.d_dig, w.desc_cap * 20));
     LBF_HIP_TRY(hipMalloc((void**)&s.d_exp, w.desc_cap * 20));
     LBF_HIP_TRY(hipMalloc((void**)&s.d_ver, w.desc_cap));
-    LBF_HIP_TRY(hipHostMalloc((void**)&s.h_data, w.slot_bytes, hipHostMallocDefault));
     LBF_HIP_TRY(hipHostMalloc((void**)&s.h_off, w.desc_cap * 8, hipHostMallocDefault));
     LBF_HIP_TRY(hipHostMalloc((void**)&s.h_size, w.desc_cap * 4, hipHostMallocDefault));
     LBF_HIP_TRY(hipHostMalloc((void**)&s.h_dig, w.desc_cap * 20, hipHostMallocDefault));
@@ -373,6 +398,17 @@ int run_oversize(Worker& w, const Job& job, uint64_t i) {
 // while the host stages the next group into the other slot.
 int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
   LBF_HIP_TRY(hipSetDevice(w.device));
+  {
+    // staging sized to the byte range this worker covers (capped at slot_max)
+    uint64_t lo = UINT64_MAX, hi = 0;
+    for (uint64_t k = begin; k < end; ++k)
+      if ((uint64_t)job.sizes[k] + 15 <= w.slot_max) {
+        lo = std::min(lo, job.offsets[k]);
+        hi = std::max(hi, job.offsets[k] + job.sizes[k]);
+      }
+    if (end > begin)
+      if (int rc = ensure_slot_bytes(w, std::min(hi > lo ? hi - lo : 0, w.slot_max) + 16)) return rc;
+  }
   int cur = 0;
   uint64_t i = begin;
   int rc = LBF_OK;

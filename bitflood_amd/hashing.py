@@ -17,6 +17,7 @@ All hashing runs on the GPU; there is no CPU path in this module.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import numpy as np
 
@@ -122,6 +123,35 @@ class ChunkHasher:
         base = buf.ctypes.data if buf.size else ctypes.addressof(ctypes.c_uint8(0))
         check(self._lib.lbf_verify_batch(self._h, base, buf.size, offs.ctypes.data, szs.ctypes.data, n,
                                          exp.ctypes.data, ver.ctypes.data, LBF_HOST_PTR))
+        return ver.astype(bool)
+
+    # -- chunks read straight from a file (lbf_file_ranges) ---------------------
+    def hash_file(self, path: str, offsets, sizes) -> np.ndarray:
+        """Digests of byte ranges of a file, pread into pinned staging: EncodeFile's
+        fread -> Base64Encode loop (Encoder.cpp:54-72) as one call."""
+        offs = np.ascontiguousarray(offsets, dtype=np.uint64)
+        szs = np.ascontiguousarray(sizes, dtype=np.uint32)
+        if offs.shape != szs.shape:
+            raise ValueError("offsets and sizes differ in length")
+        out = np.zeros((offs.size, DIGEST), dtype=np.uint8)
+        if offs.size:
+            check(self._lib.lbf_file_ranges(self._h, os.fsencode(path), offs.ctypes.data, szs.ctypes.data,
+                                            offs.size, None, out.ctypes.data))
+        return out
+
+    def verify_file(self, path: str, offsets, sizes, expected) -> np.ndarray:
+        """Resume verify of a file (Flood.cpp:259-275): True where the chunk is present
+        in full and matches; short or missing chunks are False, as the reference leaves
+        them '0'."""
+        offs = np.ascontiguousarray(offsets, dtype=np.uint64)
+        szs = np.ascontiguousarray(sizes, dtype=np.uint32)
+        exp = np.ascontiguousarray(expected, dtype=np.uint8).reshape(-1, DIGEST)
+        if szs.size != offs.size or exp.shape[0] != offs.size:
+            raise ValueError("offsets, sizes and expected differ in length")
+        ver = np.zeros(offs.size, dtype=np.uint8)
+        if offs.size:
+            check(self._lib.lbf_file_ranges(self._h, os.fsencode(path), offs.ctypes.data, szs.ctypes.data,
+                                            offs.size, exp.ctypes.data, ver.ctypes.data))
         return ver.astype(bool)
 
     def sha1(self, data) -> bytes:

@@ -217,3 +217,25 @@ def test_c2_full_size_device_resident(variant, golden, oracle):
         buf.free()
         dig.free()
         ver.free()
+
+
+def test_hash_and_verify_file(hasher, oracle, tmp_path):
+    """lbf_file_ranges through the Python face: EncodeFile's fread loop
+    (Encoder.cpp:54-72) and the resume verify (Flood.cpp:259-275) on a real file,
+    including a truncated copy (short chunks verify False) and a missing file."""
+    data = oracle.synth(31, 0, (9 << 20) + 777)
+    path = tmp_path / "f.bin"
+    path.write_bytes(data.tobytes())
+    offs, sizes = chunk_table(data.size, 262144)
+    want = oracle.sha1_batch(data, offs, sizes)
+    got = hasher.hash_file(str(path), offs, sizes)
+    assert np.array_equal(got, want)
+    assert hasher.verify_file(str(path), offs, sizes, want).all()
+    cut = 5 * 262144 + 100
+    short = tmp_path / "short.bin"
+    short.write_bytes(data[:cut].tobytes())
+    v = hasher.verify_file(str(short), offs, sizes, want)
+    assert v.tolist() == [True] * 5 + [False] * (offs.size - 5)
+    assert not hasher.verify_file(str(tmp_path / "missing.bin"), offs, sizes, want).any()
+    with pytest.raises(Exception):
+        hasher.hash_file(str(short), offs, sizes)
