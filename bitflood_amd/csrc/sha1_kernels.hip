@@ -18,6 +18,7 @@
 // Kernel "pc4/b64" (variants 7, 8): pc4 with the schedule read as uint2 pairs (8: one ds_read_b64 each).
 // Kernel "pcx4" (variant 9): two pc4-style pairs per CU, one producer each, K split, for 16-32 K chains.
 // Kernel "pcx5" (variant 10): pcx4 with words 0..15 taken by the consumer from the raw block, for 16-32 K chains.
+// Kernel "lds2" (variant 11): lds fetching whole 128-byte lines per lane, for > 32 K chains.
 #include <hip/hip_runtime.h>
 
 #include <atomic>
@@ -1282,6 +1283,71 @@ __global__ void __launch_bounds__(256) sha1_lds_kernel(ChunkParams p) {
 }
 constexpr int kLdsStages = 2;
 
+// ---------------------------------------------------------------------------
+// Kernel "lds2" (variant 11): `lds` fetching each chain's bytes a whole 128-B
+// line at a time.
+//
+// `lds` DMAs one 64-byte block per lane per step, so the two halves of a 128-B
+// line are requested one step (≈2 M other lines chip-wide at C3) apart and
+// HBM traffic reads 1.14 x algorithmic at 262 K chains (profiles/r01/c3_lds).
+// Here the DMA for blocks 2j and 2j+1 goes out as 8 back-to-back instructions,
+// so the second half merges with the first half's fill.  4 block slots per
+// wave (16 KiB): 2 workgroups per CU, 2 waves per SIMD, which still keeps the
+// VALU busy.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void lds2_dma_pair(const ChainInfo& c, uint32_t pair, uint32_t wave_lds) {
+#pragma unroll
+  for (uint32_t h = 0; h < 2; ++h) {
+    const uint32_t b = 2 * pair + h;
+    const bool ok = c.aligned && b < c.nfull;
+    const uint8_t* src = ok ? c.src + 64ull * b : reinterpret_cast<const uint8_t*>(g_pc_dummy);
+    const uint32_t slot = wave_lds + (b % 4) * (kPcRawU4 * 16);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) dma16(src + 16 * j, slot + j * (kPcLanes * 16));
+  }
+}
+
+template <bool kUniform>
+__global__ void __launch_bounds__(256) sha1_lds2_kernel(ChunkParams p) {
+  extern __shared__ __attribute__((aligned(16))) uint4 stage[];  // [wave][4 blocks][4][64]
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const ChainInfo c = chain_info<kUniform>(p, i);
+  uint4* mine = stage + wave * (4 * kPcRawU4);
+  const uint32_t wave_lds = (uint32_t)reinterpret_cast<uintptr_t>(mine);
+  const uint32_t nsteps = __builtin_amdgcn_readfirstlane(wave_max(c.nfull));
+  const bool any_unaligned = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(__ballot(c.total != 0 && !c.aligned) != 0));
+  Digest s;
+  s.init();
+  lds2_dma_pair(c, 0, wave_lds);
+  lds2_dma_pair(c, 1, wave_lds);
+  for (uint32_t k = 0; k < nsteps; ++k) {
+    // pair k/2 has landed once only pair k/2 + 1 (8 DMAs) is pending
+    if ((k & 1u) == 0) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    const uint4* raw = mine + (k % 4) * kPcRawU4 + lane;
+    uint32_t w[16];
+    block_from_vec(w, raw[0], raw[kPcLanes], raw[2 * kPcLanes], raw[3 * kPcLanes]);
+    if (any_unaligned && !c.aligned && k < c.nfull) {
+      load_words_any(w, c.src + 64ull * k, 64);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) w[q] = bswap(w[q]);
+    }
+    if (k & 1u) {
+      // both slots of pair k/2 are read: refill them with pair k/2 + 2
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      lds2_dma_pair(c, (k >> 1) + 2, wave_lds);
+    }
+    if (k < c.nfull) compress(s, w);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA outlives the wave
+  if (i >= p.n) return;
+  finish(s, c.src + 64ull * c.nfull, c.size & 63u, c.size);
+  write_result(p, i, s);
+}
+constexpr int kLds2Bytes = 4 * 4 * kPcRawU4 * 16;  // 4 waves x 16 KiB
+
 // Counter-mode splitmix64 fill, 16 bytes per thread per step.
 __global__ void __launch_bounds__(256) fill_synth_kernel(uint8_t* dst, uint64_t len, uint64_t seed,
                                                          uint64_t start_word) {
@@ -1331,9 +1397,11 @@ int pick_variant(uint64_t n) {
     // profiles/r01/sweep_v5_pcx4_ksplit.log, sweep_v9_pcx5_k40_k48.log,
     // sweep_pcx5_k48_k56_k64.log).  Many chains: every SIMD is busy
     // and the fused one-chunk-per-lane kernel issues the fewest instructions in
-    // total, LDS-staged (3).  Crossovers from tools/sweep_variants.py
-    // (profiles/r01/sweep_v123.log, sweep_v245.log, sweep_v46_pc4.log).
-    variant = n <= kPc4MaxChains ? 7 : (n <= kPcMaxChains ? 10 : 3);
+    // total, LDS-staged and fetching whole 128-byte lines (11; 2 % ahead of the
+    // per-block DMA of 3 at C3, traffic 1.14 -> 1.001 x, sweep_v3_v11_lds2.log).
+    // Crossovers from tools/sweep_variants.py (profiles/r01/sweep_v123.log,
+    // sweep_v245.log, sweep_v46_pc4.log).
+    variant = n <= kPc4MaxChains ? 7 : (n <= kPcMaxChains ? 10 : 11);
   }
   return variant;
 }
@@ -1396,6 +1464,17 @@ int launch_chunks(const ChunkParams& p, hipStream_t stream) {
     launch_pcx4<kPx4KFrom>(p, stream);
   } else if (variant == 10) {
     launch_pcx5<kPx5KFrom>(p, stream);
+  } else if (variant == 11) {
+    static std::once_flag once;
+    std::call_once(once, [] {
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_lds2_kernel<false>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, kLds2Bytes);
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_lds2_kernel<true>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, kLds2Bytes);
+    });
+    const uint32_t blocks = (p.n + 255) / 256;
+    if (p.offsets) hipLaunchKernelGGL(sha1_lds2_kernel<false>, dim3(blocks), dim3(256), kLds2Bytes, stream, p);
+    else hipLaunchKernelGGL(sha1_lds2_kernel<true>, dim3(blocks), dim3(256), kLds2Bytes, stream, p);
   } else if (variant == 3) {
     const uint32_t blocks = (p.n + 255) / 256;
     constexpr int lds = 4 * kLdsStages * kPcRawU4 * 16;
@@ -1472,7 +1551,7 @@ extern "C" int lbf_sha1_uniform_launch(const uint8_t* d_base, uint64_t len, uint
 }
 
 extern "C" int lbf_set_kernel_variant(int variant) {
-  if (variant < 0 || variant > 10) return fail(LBF_ERR_INVALID, "unknown kernel variant");
+  if (variant < 0 || variant > 11) return fail(LBF_ERR_INVALID, "unknown kernel variant");
   lbf::g_variant.store(variant);
   return LBF_OK;
 }

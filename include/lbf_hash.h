@@ -123,7 +123,7 @@ int lbf_sha1_uniform_launch(const uint8_t* d_base, uint64_t len, uint32_t chunk_
                             const uint8_t* d_expected, uint8_t* d_verdicts, void* stream);
 /* Kernel variant selection for the two launchers above (0 = automatic):
  * 1 lane, 2 pc, 3 lds, 4 pc2, 5 pcx2, 6 pc4, 7/8 pc4 with the schedule
- * read as 8-byte pairs, 9 pcx4, 10 pcx5.  Exposed for benchmarking and tests; see
+ * read as 8-byte pairs, 9 pcx4, 10 pcx5, 11 lds2.  Exposed for benchmarking and tests; see
  * DESIGN.md "kernels".  lbf_kernel_for(n) is the variant a launch of n
  * chunks runs under the current setting. */
 int lbf_set_kernel_variant(int variant);

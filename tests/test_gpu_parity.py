@@ -28,11 +28,12 @@ SEED_C = 0x5EED
 # 8-byte pairs (7: the compiler may pair the loads; 8: one ds_read_b64 each),
 # 9 = two pc4-style pairs per CU with one producer each and the round
 # constants split between consumer and producer ("pcx4"), 10 = pcx4 with
-# words 0..15 read by the consumer from the raw block ("pcx5")
-VARIANTS = [1, 2, 3, 4, 5, 6, 7, 8, 9, 10]
+# words 0..15 read by the consumer from the raw block ("pcx5"), 11 = lds fetching
+# whole 128-byte lines ("lds2")
+VARIANTS = [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11]
 
 
-@pytest.fixture(params=VARIANTS, ids=lambda v: {1: "lane", 2: "pc", 3: "lds", 4: "pc2", 5: "pcx2", 6: "pc4", 7: "pc4b64x2", 8: "pc4b64", 9: "pcx4", 10: "pcx5"}[v])
+@pytest.fixture(params=VARIANTS, ids=lambda v: {1: "lane", 2: "pc", 3: "lds", 4: "pc2", 5: "pcx2", 6: "pc4", 7: "pc4b64x2", 8: "pc4b64", 9: "pcx4", 10: "pcx5", 11: "lds2"}[v])
 def variant(request):
     H.set_kernel_variant(request.param)
     yield request.param

@@ -27,7 +27,7 @@ from bitflood_amd import ChunkHasher, DeviceBuffer  # noqa: E402
 from bitflood_amd import hashing as H  # noqa: E402
 from tests.oracle_lib import Oracle  # noqa: E402
 
-VARIANTS = list(range(1, 11))
+VARIANTS = list(range(1, 12))
 THREADS = min(16, os.cpu_count() or 1)
 
 
