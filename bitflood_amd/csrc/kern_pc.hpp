@@ -1,0 +1,606 @@
+// kern_pc.hpp -- producer/consumer kernels with one 64-chain pair per
+// workgroup: "pc" (2, and pcx2 = two pairs, 5), "pc2" (4) and "pc4" (6, 7, 8),
+// the kernels for few chains (C2).
+//
+// Part of the single translation unit sha1_kernels.hip (included from there);
+// DESIGN.md §4 has the measurements behind each kernel.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "kern_common.hpp"
+
+namespace lbf {
+namespace {
+
+// ---------------------------------------------------------------------------
+// Kernel "pc" (variant 2): producer/consumer split for few chains.
+//
+// With few chunks (C2: 16,384 chains = 256 waves for 1,024 SIMDs) a lone wave
+// issues at most one VALU every ~4 cycles (tools/probe_issue.hip), so the time
+// per chunk is set by the instruction count of ONE chain.  The 64-word message
+// expansion and the byte swaps do not depend on the chain state, so a producer
+// wave on another SIMD computes them and hands the 80 expanded words per block
+// over in LDS; the consumer wave runs only the 80 rounds (5 VALU each).
+//
+// One workgroup = 64 chains = 2 waves: wave 0 consumes, wave 1 produces.  The
+// LDS ring has 2 slots of [20 uint4][64 lanes] (20 KiB each); one workgroup
+// barrier per block step separates "producer writes slot k+1" from "consumer
+// reads slot k".  The producer keeps kPcPrefetch blocks of raw chunk bytes in
+// flight in registers.  Final (padding/length) blocks are built by the
+// producer as ordinary steps, so the consumer loop is uniform.
+// ---------------------------------------------------------------------------
+// Raw bytes of block `step` of every chain into raw slot step % 4, laid out
+// [16-byte piece j][lane] so both the DMA and the later ds_read_b128 are
+// contiguous across lanes.  Always exactly 4 VMEM instructions.
+__device__ __forceinline__ void pc_dma_step(const ChainInfo& c, uint32_t step, uint32_t raw_lds) {
+  const bool ok = c.aligned && step < c.nfull;
+  const uint8_t* src = ok ? c.src + 64ull * step : reinterpret_cast<const uint8_t*>(g_pc_dummy);
+  const uint32_t slot = raw_lds + (step % kPcRawSlots) * (kPcRawU4 * 16);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) dma16(src + 16 * j, slot + j * (kPcLanes * 16));
+}
+
+template <int kRing>
+__device__ __forceinline__ void pc_produce(uint4* ring, const ChainInfo& c, uint32_t step, int lane) {
+  uint32_t w[16];
+  if (step < c.nfull) {
+    if (c.aligned) {
+      const uint4* raw = ring + kRing * kPcSlotU4 + (step % kPcRawSlots) * kPcRawU4 + lane;
+      block_from_vec(w, raw[0], raw[kPcLanes], raw[2 * kPcLanes], raw[3 * kPcLanes]);
+    } else {
+      load_words_any(w, c.src + 64ull * step, 64);
+#pragma unroll
+      for (int k = 0; k < 16; ++k) w[k] = bswap(w[k]);
+    }
+  } else {
+    // step == nfull: block with the tail bytes; step == nfull + 1: zeros + length.
+    // Steps past `total` produce don't-care words the consumer never reads.
+    final_block(w, c.src + 64ull * c.nfull, c.size & 63u, c.size, step != c.nfull);
+  }
+  expand_store(w, ring + (step % kRing) * kPcSlotU4 + lane, kPcLanes);
+}
+
+// kRing = 2 (the shipped form): the producer writes step k+1 into slot
+// (k+1) % 2 while the consumer computes step k from slot k % 2.  A 3-slot ring
+// that let the consumer prefetch step k+1 across the barrier measured 6 % slower
+// (extra VGPR traffic and LDS instructions inside the round chain).
+// kPairs consumer/producer pairs per workgroup (waves 0..kPairs-1 consume,
+// kPairs..2*kPairs-1 produce; pair q = wave % kPairs).  kPairs = 2 with 112 KiB
+// of LDS pins ONE workgroup per CU, so each of its 4 waves has a SIMD to itself
+// -- for 16 K-32 K chains, where two 2- or 3-wave workgroups per CU would put
+// a consumer and a producer on one SIMD.
+template <bool kUniform, int kRing, int kPairs = 1>
+__global__ void __launch_bounds__(128 * kPairs) sha1_pc_kernel(ChunkParams p) {
+  extern __shared__ __attribute__((aligned(16))) uint4 lds_all[];  // per pair: W[kRing][20][64] | raw[4][4][64]
+  const int lane = threadIdx.x & 63;
+  const int wave_id = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int pair = wave_id % kPairs;
+  const int wave = wave_id / kPairs;  // 0 = consumer, 1 = producer
+  uint4* ring = lds_all + pair * (pc_lds_bytes<kRing>() / 16);
+  const uint32_t i = blockIdx.x * (kPcLanes * kPairs) + pair * kPcLanes + lane;
+  const ChainInfo c = chain_info<kUniform>(p, i);
+  // Identical in every wave of the workgroup (every wave passes every
+  // barrier); readfirstlane keeps the loop bounds scalar.
+  uint32_t nsteps = __builtin_amdgcn_readfirstlane(wave_max(c.total));
+  if (kPairs > 1) {
+    __shared__ uint32_t wg_steps;
+    if (threadIdx.x == 0) wg_steps = 0;
+    __syncthreads();
+    if (lane == 0) atomicMax(&wg_steps, nsteps);
+    __syncthreads();
+    nsteps = __builtin_amdgcn_readfirstlane(wg_steps);
+  }
+  const uint32_t nbarriers = nsteps;  // both waves pass exactly nsteps barriers
+  constexpr uint32_t kAhead = kRing - 1;  // steps the producer runs ahead
+#ifdef LBF_PC_STAMPS
+  unsigned long long acc[4] = {0, 0, 0, 0}, t0 = 0, t1 = 0, t2 = 0, t3 = 0;
+#endif
+
+  if (wave == 1) {
+    // ---------------- producer ----------------
+    const uint32_t raw_lds = (uint32_t)reinterpret_cast<uintptr_t>(ring + kRing * kPcSlotU4);
+#pragma unroll
+    for (uint32_t s = 0; s < kPcRawSlots; ++s) pc_dma_step(c, s, raw_lds);
+    // steps 0 .. kAhead-1 before the first barrier, then step k + kAhead in interval k
+    for (uint32_t k = 0; k < nbarriers + kAhead - 1; ++k) {
+      if (k < nsteps) {
+        PC_STAMP(t0);
+        // raw block k has landed once at most the 3 younger steps (12 DMAs) are pending
+        asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+        PC_STAMP(t1);
+        pc_produce<kRing>(ring, c, k, lane);
+        pc_dma_step(c, k + kPcRawSlots, raw_lds);  // reuses slot k % 4 (read above)
+        PC_STAMP(t2);
+        PC_ACC(0, t0, t1);
+        PC_ACC(1, t1, t2);
+      }
+      PC_STAMP(t2);
+      if (k + 1 >= kAhead) __syncthreads();       // barrier (k + 1 - kAhead)
+      PC_STAMP(t3);
+      PC_ACC(2, t2, t3);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA outlives the workgroup
+  } else {
+    // ---------------- consumer ----------------
+    Digest s;
+    s.init();
+    const RoundK K;
+    for (uint32_t k = 0; k < nsteps; ++k) {
+      PC_STAMP(t0);
+      __syncthreads();  // barrier k: slot k % 2 complete
+      PC_STAMP(t1);
+      if (k < c.total) compress_expanded(s, ring + (k % kRing) * kPcSlotU4 + lane, kPcLanes, K);
+      PC_STAMP(t2);
+      PC_ACC(0, t0, t1);
+      PC_ACC(1, t1, t2);
+    }
+    if (i < p.n) {
+      uint32_t be[5];
+#pragma unroll
+      for (int k = 0; k < 5; ++k) be[k] = bswap(s.h[k]);
+      if (p.digests) {
+        uint32_t* o = reinterpret_cast<uint32_t*>(p.digests + 20ull * i);
+#pragma unroll
+        for (int k = 0; k < 5; ++k) o[k] = be[k];
+      }
+      if (p.verdicts) {
+        const uint32_t* e = reinterpret_cast<const uint32_t*>(p.expected + 20ull * i);
+        uint32_t diff = 0;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) diff |= be[k] ^ e[k];
+        p.verdicts[i] = diff == 0 ? 1 : 0;
+      }
+    }
+  }
+#ifdef LBF_PC_STAMPS
+  if (lane == 0) {
+    unsigned long long* o = g_pc_stamps + (blockIdx.x * 2 * kPairs + wave_id) * 4;
+    o[0] = acc[0];
+    o[1] = acc[1];
+    o[2] = acc[2];
+    o[3] = nsteps;
+  }
+#endif
+}
+
+// ---------------------------------------------------------------------------
+// Kernel "pc2" (variant 4): one consumer, TWO producers per 64 chains.
+//
+// The consumer's round is cheapest (five VALU ops issued back to back) when
+// its schedule word already carries the round constant, leaving one v_add_u32
+// and one v_add3_u32 for the sum.  Adding K costs the producer 80 more ops per
+// block, more than one producer wave has to spare, so two producers alternate
+// blocks: producer X builds steps X, X+2, X+4, ... and spends two barrier
+// intervals on each (words 0..39 before the first, 40..79 before the second).
+// W ring: 3 slots (step k in slot k % 3): a slot is rewritten only after the
+// consumer has passed the barrier that ends its read.  Raw staging: 2 slots of
+// 4 KiB per producer.  LDS 76 KiB -> two workgroups per CU.
+// ---------------------------------------------------------------------------
+constexpr int kP2Ring = 3;
+constexpr int kP2Raw = 2;  // raw slots per producer
+constexpr int kP2LdsBytes = (kP2Ring * kPcSlotU4 + 2 * kP2Raw * kPcRawU4) * 16;
+
+// Raw bytes of `step` into raw slot `slot` of this producer: 4 DMA ops always.
+__device__ __forceinline__ void p2_dma(const ChainInfo& c, uint32_t step, uint32_t raw_lds, uint32_t slot) {
+  const bool ok = c.aligned && step < c.nfull;
+  const uint8_t* src = ok ? c.src + 64ull * step : reinterpret_cast<const uint8_t*>(g_pc_dummy);
+  const uint32_t base = raw_lds + slot * (kPcRawU4 * 16);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) dma16(src + 16 * j, base + j * (kPcLanes * 16));
+}
+
+// The 16 message words of `step`: full blocks from the raw slot (aligned) or
+// global memory (misaligned), final blocks built from the tail.
+__device__ __forceinline__ void p2_block(uint32_t (&w)[16], const uint4* raw, const ChainInfo& c, uint32_t step) {
+  if (step < c.nfull) {
+    if (c.aligned) {
+      block_from_vec(w, raw[0], raw[kPcLanes], raw[2 * kPcLanes], raw[3 * kPcLanes]);
+    } else {
+      load_words_any(w, c.src + 64ull * step, 64);
+#pragma unroll
+      for (int k = 0; k < 16; ++k) w[k] = bswap(w[k]);
+    }
+  } else {
+    final_block(w, c.src + 64ull * c.nfull, c.size & 63u, c.size, step != c.nfull);
+  }
+}
+
+template <bool kUniform>
+__global__ void __launch_bounds__(192) sha1_pc2_kernel(ChunkParams p) {
+  extern __shared__ __attribute__((aligned(16))) uint4 ring[];  // W[3][20][64] | raw[2][2][4][64]
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t i = blockIdx.x * kPcLanes + lane;
+  const ChainInfo c = chain_info<kUniform>(p, i);
+  const uint32_t nsteps = __builtin_amdgcn_readfirstlane(wave_max(c.total));
+#ifdef LBF_PC_STAMPS
+  unsigned long long acc[4] = {0, 0, 0, 0}, t0 = 0, t1 = 0, t2 = 0, t3 = 0;
+#endif
+
+  if (wave != 0) {
+    // ---------------- producer X = wave - 1: steps X, X+2, ... ----------------
+    const uint32_t X = wave - 1;
+    uint4* raw = ring + kP2Ring * kPcSlotU4 + X * (kP2Raw * kPcRawU4);
+    const uint32_t raw_lds = (uint32_t)reinterpret_cast<uintptr_t>(raw);
+    p2_dma(c, X, raw_lds, 0);
+    p2_dma(c, X + 2, raw_lds, 1);
+    uint32_t w[16];
+    // Interval b ends at barrier b.  Producer X finishes step b when b % 2 == X
+    // and starts step b + 1 otherwise; producer 0 builds step 0 whole.
+    for (uint32_t b = 0; b < nsteps; ++b) {
+      const bool second = (b & 1u) == X;
+      const uint32_t step = second ? b : b + 1;
+      const bool first_too = (b == 0 && X == 0);
+      PC_STAMP(t0);
+      PC_COPY(t1, t0);
+      if ((!second || first_too) && step < nsteps) {
+        const uint32_t j = (step - X) >> 1;  // this producer's j-th step
+        // block j has landed once only block j+1's 4 DMAs may be pending
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        PC_STAMP(t1);
+        p2_block(w, raw + (j & 1u) * kPcRawU4 + lane, c, step);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // raw slot read before it is refilled
+        p2_dma(c, step + 4, raw_lds, j & 1u);
+        expand_store_wk<0>(w, ring + (step % kP2Ring) * kPcSlotU4 + lane, kPcLanes);
+      }
+      if (second && step < nsteps) expand_store_wk<1>(w, ring + (step % kP2Ring) * kPcSlotU4 + lane, kPcLanes);
+      PC_STAMP(t2);
+      __syncthreads();  // barrier b
+      PC_STAMP(t3);
+      PC_ACC(0, t0, t1);
+      PC_ACC(1, t1, t2);
+      PC_ACC(2, t2, t3);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA outlives the workgroup
+  } else {
+    // ---------------- consumer ----------------
+    Digest s;
+    s.init();
+    for (uint32_t k = 0; k < nsteps; ++k) {
+      PC_STAMP(t0);
+      __syncthreads();  // barrier k: slot k % 3 complete
+      PC_STAMP(t1);
+      if (k < c.total) compress_expanded_wk(s, ring + (k % kP2Ring) * kPcSlotU4 + lane, kPcLanes);
+      PC_STAMP(t2);
+      PC_ACC(0, t0, t1);
+      PC_ACC(1, t1, t2);
+    }
+    if (i < p.n) {
+      uint32_t be[5];
+#pragma unroll
+      for (int k = 0; k < 5; ++k) be[k] = bswap(s.h[k]);
+      if (p.digests) {
+        uint32_t* o = reinterpret_cast<uint32_t*>(p.digests + 20ull * i);
+#pragma unroll
+        for (int k = 0; k < 5; ++k) o[k] = be[k];
+      }
+      if (p.verdicts) {
+        const uint32_t* e = reinterpret_cast<const uint32_t*>(p.expected + 20ull * i);
+        uint32_t diff = 0;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) diff |= be[k] ^ e[k];
+        p.verdicts[i] = diff == 0 ? 1 : 0;
+      }
+    }
+  }
+#ifdef LBF_PC_STAMPS
+  if (lane == 0) {
+    unsigned long long* o = g_pc_stamps + (blockIdx.x * 3 + wave) * 4;
+    o[0] = acc[0];
+    o[1] = acc[1];
+    o[2] = acc[2];
+    o[3] = nsteps;
+  }
+#endif
+}
+
+// ---------------------------------------------------------------------------
+// Kernel "pc4" (variant 6): pc2 with the schedule double-buffered in the
+// consumer's registers.
+//
+// pc2's consumer loads step k's 80 words after barrier k and its first round
+// waits for the first of them: an LDS round trip per step, longer while the
+// producers' writes and DMA share the LDS.  Here the producers run one step
+// further ahead (step k+1 is complete at barrier k), and right after barrier k
+// the consumer loads ALL of step k+1 into a second register set while it runs
+// step k from the set it loaded one step earlier.  The loads complete during
+// the step, so no round ever waits for LDS.  Fifteen loads go out at once (the
+// lgkm counter holds 15) and five more after the fourth quad of rounds.  The
+// step loop is unrolled by two so the sets swap roles without copies.
+//
+// Interval b ends at barrier b.  In interval b producer (b+1) % 2 writes words
+// 40..79 of step b+1 and the other one words 0..39 of step b+2; interval 0
+// also builds steps 0 and 1 whole.  Step s is in slot s % 4: its first half
+// is written after barrier s-3, and the consumer finished loading step s-4
+// from that slot before barrier s-4 (3 slots would do; the fourth costs
+// nothing and makes the slot index a mask).  LDS 96 KiB: one
+// workgroup per CU, so each of the three waves has a SIMD of its own.
+// ---------------------------------------------------------------------------
+constexpr int kPc4Ring = 4;
+// Diagnostic builds only (tools/probe_pc.hip): LBF_PC4_NOLOADS feeds the
+// rounds opaque registers instead of LDS words, LBF_PC4_NOBARRIER drops the
+// barriers.  Both give wrong digests; they isolate what loads and barriers cost.
+#ifdef LBF_PC4_NOLOADS
+#define PC4_LOAD(dst, src) asm volatile("" : "=v"((dst).x), "=v"((dst).y), "=v"((dst).z), "=v"((dst).w))
+#else
+#define PC4_LOAD(dst, src) (dst) = (src)
+#endif
+#ifdef LBF_PC4_NOBARRIER
+#define PC4_SYNC() do {} while (0)
+#else
+#define PC4_SYNC() __syncthreads()
+#endif
+constexpr int kPc4LdsBytes = (kPc4Ring * kPcSlotU4 + 2 * kP2Raw * kPcRawU4) * 16;
+constexpr int kPc4Early = 15;  // loads issued before the first round
+constexpr int kPc4LateAt = 3;  // the rest after quad 3's rounds
+
+// Step from `cur` (in registers); meanwhile the next step's 20 quads are
+// loaded from `next_slot` (this lane's column) into `nxt`.  Every lane runs
+// the rounds (no divergent branch around the late loads); a lane whose chain
+// has ended (`live` false) keeps its digest.
+__device__ __forceinline__ void pc4_compress(Digest& s, const uint4 (&cur)[kPcQuads], uint4 (&nxt)[kPcQuads],
+                                             const uint4* next_slot, bool live, bool all_live) {
+#pragma unroll
+  for (int q = 0; q < kPc4Early; ++q) PC4_LOAD(nxt[q], next_slot[q * kPcLanes]);
+  // early loads go first (fenced on the digest, not on copies of it, so the
+  // working state needs no register copies)
+  asm volatile("" : "+v"(s.h[0]), "+v"(s.h[1]), "+v"(s.h[2]), "+v"(s.h[3]), "+v"(s.h[4])::"memory");
+  uint32_t a = s.h[0], b = s.h[1], c = s.h[2], d = s.h[3], e = s.h[4];
+#pragma unroll
+  for (int q = 0; q < kPcQuads; ++q) {
+    round_step_wk(4 * q + 0, a, b, c, d, e, cur[q].x);
+    round_step_wk(4 * q + 1, a, b, c, d, e, cur[q].y);
+    round_step_wk(4 * q + 2, a, b, c, d, e, cur[q].z);
+    round_step_wk(4 * q + 3, a, b, c, d, e, cur[q].w);
+    if (q == kPc4LateAt) {
+      // The two fences pin the late loads between quads 3 and 4: rounds are
+      // ordered through the state, loads through the memory clobber (left
+      // alone, the compiler sinks them to the end of the step, right before
+      // the barrier, which then waits for them).
+      asm volatile("" : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+v"(e)::"memory");
+#pragma unroll
+      for (int r = kPc4Early; r < kPcQuads; ++r) PC4_LOAD(nxt[r], next_slot[r * kPcLanes]);
+      asm volatile("" : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+v"(e)::"memory");
+    }
+  }
+  if (all_live) {  // wave-uniform: every chain of the workgroup has this step
+    s.h[0] += a;
+    s.h[1] += b;
+    s.h[2] += c;
+    s.h[3] += d;
+    s.h[4] += e;
+  } else {
+    s.h[0] = live ? s.h[0] + a : s.h[0];
+    s.h[1] = live ? s.h[1] + b : s.h[1];
+    s.h[2] = live ? s.h[2] + c : s.h[2];
+    s.h[3] = live ? s.h[3] + d : s.h[3];
+    s.h[4] = live ? s.h[4] + e : s.h[4];
+  }
+}
+
+// pc4_compress with the schedule read as 40 ds_read_b64 (variant 7).  A lone
+// wave pays ≈96 cycles per block for 20 ds_read_b128 over the same rounds fed
+// from registers, and ≈4 for 40 ds_read_b64 (tools/probe_lds_lanes.hip,
+// profiles/r01/probe_lds_lanes.log).  The lgkm counter holds 15, so the next
+// step's 40 pairs go out in three batches: before round 0, after round 16 and
+// after round 40, each pinned by fences like the late loads of pc4_compress.
+constexpr int kPc5Pairs = 40;
+constexpr int kPc5B1 = 15, kPc5B1At = 7;   // pairs 0..14 first; 15..27 after pair 7's rounds
+constexpr int kPc5B2 = 28, kPc5B2At = 19;  // pairs 28..39 after pair 19's rounds
+// kSplit keeps every load a single ds_read_b64: a memory fence between loads
+// stops the compiler from pairing them into ds_read2st64_b64 (which returns
+// four VGPRs per lane, like ds_read_b128).
+template <bool kSplit>
+__device__ __forceinline__ void pc5_load(uint2& dst, const uint2* base, int q) {
+  if (kSplit) asm volatile("" ::: "memory");  // the pairing pass does not look across it
+  dst = base[q * kPcLanes];
+}
+template <bool kSplit>
+__device__ __forceinline__ void pc5_compress(Digest& s, const uint2 (&cur)[kPc5Pairs], uint2 (&nxt)[kPc5Pairs],
+                                             const uint2* next_slot, bool live, bool all_live) {
+#pragma unroll
+  for (int q = 0; q < kPc5B1; ++q) pc5_load<kSplit>(nxt[q], next_slot, q);
+  asm volatile("" : "+v"(s.h[0]), "+v"(s.h[1]), "+v"(s.h[2]), "+v"(s.h[3]), "+v"(s.h[4])::"memory");
+  uint32_t a = s.h[0], b = s.h[1], c = s.h[2], d = s.h[3], e = s.h[4];
+#pragma unroll
+  for (int q = 0; q < kPc5Pairs; ++q) {
+    round_step_wk(2 * q + 0, a, b, c, d, e, cur[q].x);
+    round_step_wk(2 * q + 1, a, b, c, d, e, cur[q].y);
+    if (q == kPc5B1At || q == kPc5B2At) {
+      asm volatile("" : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+v"(e)::"memory");
+      const int lo = q == kPc5B1At ? kPc5B1 : kPc5B2;
+      const int hi = q == kPc5B1At ? kPc5B2 : kPc5Pairs;
+#pragma unroll
+      for (int r = lo; r < hi; ++r) pc5_load<kSplit>(nxt[r], next_slot, r);
+      asm volatile("" : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+v"(e)::"memory");
+    }
+  }
+  if (all_live) {
+    s.h[0] += a;
+    s.h[1] += b;
+    s.h[2] += c;
+    s.h[3] += d;
+    s.h[4] += e;
+  } else {
+    s.h[0] = live ? s.h[0] + a : s.h[0];
+    s.h[1] = live ? s.h[1] + b : s.h[1];
+    s.h[2] = live ? s.h[2] + c : s.h[2];
+    s.h[3] = live ? s.h[3] + d : s.h[3];
+    s.h[4] = live ? s.h[4] + e : s.h[4];
+  }
+}
+
+// The consumer's side of one pc4 step in either layout: uint4 quads (kVec 4,
+// variant 6) or uint2 pairs (kVec 2, variant 7) of the same 20 KiB slot.
+template <int kVec>
+struct Pc4Sched;
+template <>
+struct Pc4Sched<4> {
+  uint4 v[kPcQuads];
+  static __device__ __forceinline__ const uint4* col(const uint4* ring, int slot, int lane) {
+    return ring + slot * kPcSlotU4 + lane;
+  }
+  __device__ __forceinline__ void load_all(const uint4* src) {
+#pragma unroll
+    for (int q = 0; q < kPcQuads; ++q) v[q] = src[q * kPcLanes];
+  }
+};
+template <int kVec>
+struct Pc4Sched {  // kVec 2: uint2 pairs, loads may pair up; kVec 1: single ds_read_b64 each
+  uint2 v[kPc5Pairs];
+  static __device__ __forceinline__ const uint2* col(const uint4* ring, int slot, int lane) {
+    return reinterpret_cast<const uint2*>(ring + slot * kPcSlotU4) + lane;
+  }
+  __device__ __forceinline__ void load_all(const uint2* src) {
+#pragma unroll
+    for (int q = 0; q < kPc5Pairs; ++q) v[q] = src[q * kPcLanes];
+  }
+};
+__device__ __forceinline__ void pc4_step(Digest& s, const Pc4Sched<4>& cur, Pc4Sched<4>& nxt, const uint4* next_slot,
+                                         bool live, bool all_live) {
+  pc4_compress(s, cur.v, nxt.v, next_slot, live, all_live);
+}
+template <int kVec>
+__device__ __forceinline__ void pc4_step(Digest& s, const Pc4Sched<kVec>& cur, Pc4Sched<kVec>& nxt,
+                                         const uint2* next_slot, bool live, bool all_live) {
+  pc5_compress<kVec == 1>(s, cur.v, nxt.v, next_slot, live, all_live);
+}
+
+// Producer side: half kHalf of step `step` into its slot, in the kVec layout.
+template <int kVec, int kHalf>
+__device__ __forceinline__ void pc4_store_half(uint32_t (&w)[16], uint4* ring, uint32_t step, int lane) {
+  uint4* slot = ring + (step % 4) * kPcSlotU4;
+  if (kVec == 4) expand_store_wk<kHalf>(w, slot + lane, kPcLanes);
+  else expand_store_wk2<kHalf>(w, reinterpret_cast<uint2*>(slot) + lane, kPcLanes);
+}
+
+// A barrier the consumer's rounds cannot cross: the compiler may otherwise move
+// register-only round code over __syncthreads (it orders memory only), which
+// put a barrier right behind a fresh batch of loads and made it wait for them.
+#ifdef LBF_PC_STAMPS
+#define PC4_ACC_ARGS , unsigned long long (&acc)[4]
+#else
+#define PC4_ACC_ARGS
+#endif
+__device__ __forceinline__ void pc4_barrier(Digest& s PC4_ACC_ARGS) {
+  asm volatile("" : "+v"(s.h[0]), "+v"(s.h[1]), "+v"(s.h[2]), "+v"(s.h[3]), "+v"(s.h[4])::"memory");
+#ifdef LBF_PC_STAMPS
+  unsigned long long t0 = 0, t1 = 0;
+  PC_STAMP(t0);
+#endif
+  PC4_SYNC();
+#ifdef LBF_PC_STAMPS
+  PC_STAMP(t1);
+  PC_ACC(0, t0, t1);
+#endif
+  asm volatile("" : "+v"(s.h[0]), "+v"(s.h[1]), "+v"(s.h[2]), "+v"(s.h[3]), "+v"(s.h[4])::"memory");
+}
+
+template <bool kUniform, int kVec>
+__global__ void __launch_bounds__(192) sha1_pc4_kernel(ChunkParams p) {
+  extern __shared__ __attribute__((aligned(16))) uint4 ring[];  // W[3][20][64] | raw[2][2][4][64]
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t i = blockIdx.x * kPcLanes + lane;
+  const ChainInfo c = chain_info<kUniform>(p, i);
+  const uint32_t nsteps = __builtin_amdgcn_readfirstlane(wave_max(c.total));
+#ifdef LBF_PC_STAMPS
+  unsigned long long acc[4] = {0, 0, 0, 0}, t0 = 0, t1 = 0, t2 = 0;
+#define PC4_ACC , acc
+#else
+#define PC4_ACC
+#endif
+
+  if (wave != 0) {
+    // ---------------- producer X = wave - 1: steps X, X+2, ... ----------------
+    const uint32_t X = wave - 1;
+    uint4* raw = ring + kPc4Ring * kPcSlotU4 + X * (kP2Raw * kPcRawU4);
+    const uint32_t raw_lds = (uint32_t)reinterpret_cast<uintptr_t>(raw);
+    p2_dma(c, X, raw_lds, 0);
+    p2_dma(c, X + 2, raw_lds, 1);
+    uint32_t w[16];
+    // words 0..39 of this producer's step `step` (its j-th); the raw slot is
+    // refilled with step + 4
+    auto first_half = [&](uint32_t step) {
+      const uint32_t j = (step - X) >> 1;
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // block j landed; only j+1's DMAs pending
+      p2_block(w, raw + (j & 1u) * kPcRawU4 + lane, c, step);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // raw slot read before it is refilled
+      p2_dma(c, step + 4, raw_lds, j & 1u);
+      pc4_store_half<kVec, 0>(w, ring, step, lane);
+    };
+    for (uint32_t b = 0; b < nsteps; ++b) {
+      PC_STAMP(t0);
+      if (b == 0 && X == 0) {  // prologue: step 0 whole
+        first_half(0);
+        pc4_store_half<kVec, 1>(w, ring, 0, lane);
+      }
+      const uint32_t fin = b + 1;  // finished in interval b by producer fin % 2
+      if ((fin & 1u) == X && fin < nsteps) {
+        if (b == 0) first_half(fin);
+        pc4_store_half<kVec, 1>(w, ring, fin, lane);
+      }
+      const uint32_t start = b + 2;  // started in interval b by producer start % 2
+      if ((start & 1u) == X && start < nsteps) first_half(start);
+      PC_STAMP(t1);
+      PC4_SYNC();  // barrier b: steps <= b + 1 complete
+      PC_STAMP(t2);
+      PC_ACC(1, t0, t1);
+      PC_ACC(2, t1, t2);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA outlives the workgroup
+  } else {
+    // ---------------- consumer ----------------
+    Digest s;
+    s.init();
+    Pc4Sched<kVec> A, B;
+    // steps every chain of the workgroup has (inactive lanes count as having all)
+    const uint32_t min_steps =
+        __builtin_amdgcn_readfirstlane(wave_min(i < p.n ? c.total : 0xFFFFFFFFu));
+    if (nsteps > 0) {
+      PC4_SYNC();  // barrier 0: steps 0 and 1 complete
+      A.load_all(Pc4Sched<kVec>::col(ring, 0, lane));
+      // Once, so that the loop's first rounds need no wait on either path into
+      // it (otherwise every iteration waits for its own first load).
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+    }
+    uint32_t k = 0;
+    // Four steps per iteration while every chain of the workgroup is running
+    // and every step is followed by a barrier: k % 4 == 0, so the slots are
+    // compile-time offsets and the steps need no liveness checks.
+    for (; k + 4 <= min_steps && k + 4 < nsteps; k += 4) {
+      pc4_step(s, A, B, Pc4Sched<kVec>::col(ring, 1, lane), true, true);
+      pc4_barrier(s PC4_ACC);  // barrier k+1
+      pc4_step(s, B, A, Pc4Sched<kVec>::col(ring, 2, lane), true, true);
+      pc4_barrier(s PC4_ACC);  // barrier k+2
+      pc4_step(s, A, B, Pc4Sched<kVec>::col(ring, 3, lane), true, true);
+      pc4_barrier(s PC4_ACC);  // barrier k+3
+      pc4_step(s, B, A, Pc4Sched<kVec>::col(ring, 0, lane), true, true);
+      pc4_barrier(s PC4_ACC);  // barrier k+4
+    }
+    for (; k < nsteps; k += 2) {
+      // after barrier k: steps <= k+1 complete; A holds step k
+      pc4_step(s, A, B, Pc4Sched<kVec>::col(ring, (k + 1) % kPc4Ring, lane), k < c.total, k < min_steps);
+      if (k + 1 >= nsteps) break;
+      pc4_barrier(s PC4_ACC);  // barrier k+1
+      pc4_step(s, B, A, Pc4Sched<kVec>::col(ring, (k + 2) % kPc4Ring, lane), k + 1 < c.total, k + 1 < min_steps);
+      if (k + 2 >= nsteps) break;
+      pc4_barrier(s PC4_ACC);  // barrier k+2
+    }
+    if (i < p.n) write_result(p, i, s);
+  }
+#ifdef LBF_PC_STAMPS
+  if (lane == 0) {
+    unsigned long long* o = g_pc_stamps + (blockIdx.x * 3 + wave) * 4;
+    o[0] = acc[0];  // consumer: cycles at barriers
+    o[1] = acc[1];  // producer: work
+    o[2] = acc[2];  // producer: barrier
+    o[3] = nsteps;
+  }
+#endif
+#undef PC4_ACC
+}
+
+}  // namespace
+}  // namespace lbf
