@@ -67,3 +67,17 @@ def test_no_gpu_fails_loudly():
 def test_kernels_compiled_for_gfx950():
     blob = open(_capi.LIB_PATH, "rb").read()
     assert b"amdgcn-amd-amdhsa--gfx950" in blob
+
+
+def test_header_is_plain_c(tmp_path):
+    """include/lbf_hash.h compiles as C99 with warnings as errors, links against
+    liblbfhash.so from a C program, and behaves (tests/c/c_abi_check.c)."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = tmp_path / "c_abi_check"
+    libdir = os.path.dirname(_capi.LIB_PATH)
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Wextra", "-Werror", "-pedantic",
+                    "-I", os.path.join(root, "include"), os.path.join(root, "tests", "c", "c_abi_check.c"),
+                    "-L", libdir, "-llbfhash", f"-Wl,-rpath,{libdir}", "-o", str(exe)], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, (r.returncode, r.stdout, r.stderr)
+    assert r.stdout.startswith("ok:")
