@@ -303,7 +303,11 @@ struct Source {
     constexpr uint64_t kMinPart = 8ull << 20;
     const uint64_t parts = std::min<uint64_t>(threads, len / kMinPart);
     if (parts <= 1) return read_serial(dst, off, len);
-    const uint64_t step = (len / parts + 4095) & ~4095ull;
+    // ceil(len / parts), rounded up to a page: parts * step must cover len.
+    // (Rounding floor(len / parts) instead left the last len % parts bytes
+    // uncopied whenever floor(len / parts) was already a page multiple; found
+    // by tools/fuzz_gpu.py, regression test test_staging_split_covers_tail.)
+    const uint64_t step = ((len + parts - 1) / parts + 4095) & ~4095ull;
     std::vector<uint64_t> got(parts, 0), want(parts, 0);
     std::vector<std::thread> th;
     for (uint64_t p = 0; p < parts; ++p) {

@@ -240,3 +240,19 @@ def test_hash_and_verify_file(hasher, oracle, tmp_path):
     assert not hasher.verify_file(str(tmp_path / "missing.bin"), offs, sizes, want).any()
     with pytest.raises(Exception):
         hasher.hash_file(str(short), offs, sizes)
+
+
+@pytest.mark.parametrize("extra", [1, 2, 4095, 4097])
+def test_staging_split_covers_tail(hasher, oracle, extra):
+    """A staging group of 3 x 8 MiB + `extra` bytes is copied by 3 host threads;
+    the split must cover the tail bytes (floor(len/3) is a page multiple for
+    small `extra`, which once left the last bytes uncopied: hash mode failed with
+    LBF_ERR_IO and verify mode returned false mismatches).  Found by
+    tools/fuzz_gpu.py seed 23006099."""
+    n = 3 * (8 << 20) + extra
+    data = oracle.synth(57, 0, n)
+    offs = np.array([0, n - 100, 5], dtype=np.uint64)
+    sizes = np.array([n, 100, n - 5], dtype=np.uint32)
+    want = oracle.sha1_batch(data, offs, sizes)
+    assert np.array_equal(hasher.hash_chunks(data, offs, sizes), want)
+    assert hasher.verify_chunks(data, offs, sizes, want).all()

@@ -90,14 +90,60 @@ def one_case(seed, orc, hasher, pool):
     return v, mode, n, bool(np.array_equal(ver, ~bad))
 
 
+def replay(seed, orc, hasher, pool, repeats):
+    """Re-run one failing case and say where it differs: hash vs verify, which
+    chunks, their sizes and alignment, whether other variants agree, and whether
+    the result repeats."""
+    rng = np.random.default_rng(seed)
+    v = int(rng.choice(VARIANTS))
+    mode = int(rng.integers(0, 3))
+    print(json.dumps({"seed": seed, "variant": v, "mode": mode}), flush=True)
+    if mode == 2:
+        print("uniform-mode replay: rerun one_case", one_case(seed, orc, hasher, pool), flush=True)
+        return
+    n = int(rng.integers(1, 6000))
+    sizes, kind = draw_sizes(rng, n)
+    offs = np.array([rng.integers(0, pool.size - int(s) + 1) for s in sizes], dtype=np.uint64)
+    if rng.random() < 0.5:
+        offs &= ~np.uint64(15)
+    want = orc.sha1_batch(pool, offs, sizes, nthreads=THREADS)
+    exp = want.copy()
+    bad = np.zeros(n, bool)
+    if mode == 1:
+        bad = rng.random(n) < 0.1
+        exp[bad, rng.integers(0, 20)] ^= np.uint8(1 << int(rng.integers(0, 8)))
+    print(json.dumps({"n": n, "kind": kind, "aligned16": int((offs % 16 == 0).sum()),
+                      "size_min": int(sizes.min()), "size_max": int(sizes.max())}), flush=True)
+    for vv in [v] + [x for x in VARIANTS if x != v]:
+        H.set_kernel_variant(vv)
+        for r in range(repeats if vv == v else 1):
+            got = hasher.hash_chunks(pool, offs, sizes)
+            hbad = np.nonzero((got != want).any(axis=1))[0]
+            ver = hasher.verify_chunks(pool, offs, sizes, exp)
+            vbad = np.nonzero(ver != ~bad)[0]
+            info = {"variant": vv, "rep": r, "hash_mismatch": hbad[:8].tolist(), "n_hash_mismatch": int(hbad.size),
+                    "verify_mismatch": vbad[:8].tolist(), "n_verify_mismatch": int(vbad.size)}
+            for k in list(hbad[:3]) + list(vbad[:3]):
+                info[f"chunk{k}"] = {"size": int(sizes[k]), "off_mod16": int(offs[k] % 16), "corrupted": bool(bad[k]),
+                                     "group_pos": int(k % 128)}
+            print(json.dumps(info), flush=True)
+    H.set_kernel_variant(0)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seconds", type=float, default=90)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cases", type=int, default=1 << 30)
+    ap.add_argument("--replay", type=int, default=None, help="re-run one case seed with diagnostics")
+    ap.add_argument("--repeats", type=int, default=3)
     a = ap.parse_args()
     orc = Oracle()
     pool = orc.synth(0xF022, 0, 160 << 20, nthreads=THREADS)
+    if a.replay is not None:
+        with ChunkHasher(device_mask=1) as hasher:
+            replay(a.replay, orc, hasher, pool, a.repeats)
+        return 0
     t0 = time.time()
     k = 0
     stats = {}
