@@ -449,7 +449,9 @@ int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
       const uint64_t o = job.offsets[i + k];
       s.h_off[k] = o - lo + shift;
       s.h_size[k] = job.sizes[i + k];
-      s.h_ok[k] = (o + job.sizes[i + k] <= lo + avail) ? 1 : 0;
+      // An empty chunk is always readable, wherever it lies: the reference's
+      // fseek succeeds past EOF and fread of 0 bytes returns 0 (Flood.cpp:259-275).
+      s.h_ok[k] = (job.sizes[i + k] == 0 || o + job.sizes[i + k] <= lo + avail) ? 1 : 0;
     }
     const uint64_t copy_bytes = avail + shift;
     LBF_HIP_TRY(hipMemcpyAsync(s.d_data, s.h_data, copy_bytes, hipMemcpyHostToDevice, s.stream));

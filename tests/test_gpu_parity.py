@@ -256,3 +256,17 @@ def test_staging_split_covers_tail(hasher, oracle, extra):
     want = oracle.sha1_batch(data, offs, sizes)
     assert np.array_equal(hasher.hash_chunks(data, offs, sizes), want)
     assert hasher.verify_chunks(data, offs, sizes, want).all()
+
+
+def test_verify_file_empty_chunk_past_eof(hasher, tmp_path):
+    """Flood.cpp:259-275: fseek past EOF succeeds and fread of 0 bytes returns 0,
+    so an empty chunk past the end of an existing file verifies ('1'); with no file
+    (fopen fails) nothing does."""
+    path = tmp_path / "short.bin"
+    path.write_bytes(b"x" * 1000)
+    empty = hashlib.sha1(b"").digest()
+    offs = np.array([0, 5000, 999], dtype=np.uint64)
+    sizes = np.array([0, 0, 2], dtype=np.uint32)
+    exp = np.frombuffer(empty * 3, np.uint8).reshape(3, 20)
+    assert hasher.verify_file(str(path), offs, sizes, exp).tolist() == [True, True, False]
+    assert not hasher.verify_file(str(tmp_path / "missing.bin"), offs, sizes, exp).any()
