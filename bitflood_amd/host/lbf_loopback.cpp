@@ -191,9 +191,17 @@ void write_source(const std::string& path, U64 size, unsigned threads) {
   if (!ok) die("writing " + path + " failed");
 }
 
+// The leecher creates a file on its first received chunk (ChunkMethods.cpp:169-172),
+// so a zero-chunk (empty) file is never created: an empty seed file and a missing
+// leech file count as equal, as they would for the reference's peers.
 bool files_equal(const std::string& a, const std::string& b) {
   FILE* fa = fopen(a.c_str(), "rb");
   FILE* fb = fopen(b.c_str(), "rb");
+  if (fa && !fb) {
+    const bool empty = fgetc(fa) == EOF;
+    fclose(fa);
+    return empty;
+  }
   bool eq = fa && fb;
   std::vector<char> x(16 << 20), y(16 << 20);
   while (eq) {

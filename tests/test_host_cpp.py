@@ -97,6 +97,8 @@ def test_loopback_needs_gpu():
     (64 << 20, 262144, 64, 16, 0),                 # C5 chunk size, small file
     ((16 << 20) + 12345, 65536, 512, 128, 7),      # odd tail, wire corruption every 7th chunk
     (3 * 262144 + 1, 262144, 1, 1, 0),             # one chunk in flight, batch of one
+    (65537, 4096, 1, 3, 1),                        # every chunk corrupted on its first send
+    (0, 1000, 1024, 512, 0),                       # empty file: no chunks, nothing to create
 ])
 def test_loopback_two_peers(tmp_path, size, cs, window, batch, corrupt):
     """C5 shape: seeder and leecher over 127.0.0.1 speaking the reference's frames;
