@@ -3,6 +3,7 @@
 // reference signature, the batch extension, and the seeder/receiver verify
 // paths of Flood (ChunkMethods.cpp:89-225 restated) on a real file.
 //   lbf_gpu_tests <scratch-dir>
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -125,6 +126,48 @@ int main(int argc, char** argv) {
   again.m_rootdir = ldir;
   CHECK(again.Initialize(lf) == Error::NO_ERROR_LBF);
   CHECK(again.m_runtimefiles["copy.bin"].m_chunkmap == "1111");
+
+  // multi-file EncodeFile (Encoder.cpp:17-102): every file of m_files, an empty
+  // one included (no chunks), keyed by name; the hashes equal the batch path's
+  {
+    const std::vector<std::pair<std::string, size_t>> files = {
+        {dir + "/c.bin", 2 * 65536 + 56}, {dir + "/a.bin", 100000}, {dir + "/b.bin", 0}};
+    Encoder::ToEncode me;
+    me.m_chunksize = 65536;
+    std::vector<std::vector<U8>> bytes;
+    for (size_t k = 0; k < files.size(); ++k) {
+      bytes.push_back(pattern(files[k].second, 20 + (U32)k));
+      FILE* g = std::fopen(files[k].first.c_str(), "wb");
+      if (!bytes.back().empty()) std::fwrite(bytes.back().data(), 1, bytes.back().size(), g);
+      std::fclose(g);
+      me.m_files.push_back(files[k].first);
+    }
+    FloodFile mf;
+    CHECK(Encoder::EncodeFile(me, mf) == Error::NO_ERROR_LBF);
+    CHECK(mf.m_files.size() == 3);
+    for (size_t k = 0; k < files.size(); ++k) {
+      const FloodFile::FileSPtr& fe = mf.m_files[files[k].first];
+      const size_t n = (files[k].second + 65535) / 65536;
+      CHECK(fe && fe->m_size == files[k].second && fe->m_chunks.size() == n);
+      std::vector<U64> o(n);
+      std::vector<U32> z(n);
+      for (size_t i = 0; i < n; ++i) {
+        o[i] = 65536ull * i;
+        z[i] = (U32)std::min<size_t>(65536, files[k].second - 65536 * i);
+      }
+      V_String want;
+      if (n) CHECK(Encoder::Base64EncodeBatch(bytes[k].data(), bytes[k].size(), o.data(), z.data(), n, want) ==
+                   Error::NO_ERROR_LBF);
+      for (size_t i = 0; fe && i < n && i < fe->m_chunks.size() && i < want.size(); ++i) {
+        CHECK(fe->m_chunks[i].m_index == i && fe->m_chunks[i].m_size == z[i] && fe->m_chunks[i].m_hash == want[i]);
+      }
+    }
+    // a missing file: the call fails and the output is left as it was (:45-47, :96-99)
+    me.m_files.push_back(dir + "/missing.bin");
+    FloodFile untouched;
+    CHECK(Encoder::EncodeFile(me, untouched) == Error::UNKNOWN_ERROR_LBF);
+    CHECK(untouched.m_files.empty());
+  }
 
   if (g_fail) {
     std::fprintf(stderr, "%d check(s) failed (last error: %s)\n", g_fail, Encoder::LastError());
