@@ -270,3 +270,21 @@ def test_verify_file_empty_chunk_past_eof(hasher, tmp_path):
     exp = np.frombuffer(empty * 3, np.uint8).reshape(3, 20)
     assert hasher.verify_file(str(path), offs, sizes, exp).tolist() == [True, True, False]
     assert not hasher.verify_file(str(tmp_path / "missing.bin"), offs, sizes, exp).any()
+
+
+def test_chunk_over_512_mib_bit_length_high_word(oracle):
+    """A chunk of 2^29 bytes or more has a non-zero high word of the 64-bit bit
+    length in the final block (iterhash.h:30-31,106-121: GetBitCountHi); no
+    configuration's chunk reaches that size, so pin it once on the device path."""
+    n_bytes = (512 << 20) + 100
+    buf = DeviceBuffer(n_bytes)
+    dig = DeviceBuffer(20)
+    try:
+        buf.fill_synthetic(91)
+        H.uniform_launch(buf, n_bytes, n_bytes, 0, 1, dig)
+        H.synchronize()
+        got = dig.download(20).tobytes()
+    finally:
+        buf.free()
+        dig.free()
+    assert got == hashlib.sha1(oracle.synth(91, 0, n_bytes, nthreads=8).tobytes()).digest()
