@@ -183,7 +183,7 @@ struct Slot {
 
 struct Worker {
   int device = 0;
-  Slot slot[2];
+  std::vector<Slot> slot;  // LBF_SLOTS of them (default 3), used round-robin
   uint64_t slot_bytes = 0;  // current staging capacity per slot (grown on demand)
   uint64_t slot_max = 0;    // LBF_SLOT_MB: the largest a slot may grow
   uint64_t desc_cap = 0;
@@ -232,6 +232,10 @@ int ensure_slot_bytes(Worker& w, uint64_t need) {
 int worker_init(Worker& w, int device) {
   w.device = device;
   w.slot_max = std::max<uint64_t>(env_u64("LBF_SLOT_MB", 512) << 20, 1ull << 20);
+  // Three slots keep the PCIe link busy: with two, staging group g+2 waits for
+  // group g's H2D *and* its kernel (one chunk's serial chain, ≈3.2 ms at 256 KiB
+  // whatever the group size), so the link idles once per pair of groups.
+  w.slot.resize(std::min<uint64_t>(8, std::max<uint64_t>(2, env_u64("LBF_SLOTS", 3))));
   w.slot_bytes = 0;
   w.desc_cap = 1u << 16;
   LBF_HIP_TRY(hipSetDevice(device));
@@ -403,15 +407,22 @@ int run_oversize(Worker& w, const Job& job, uint64_t i) {
 int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
   LBF_HIP_TRY(hipSetDevice(w.device));
   {
-    // staging sized to the byte range this worker covers (capped at slot_max)
-    uint64_t lo = UINT64_MAX, hi = 0;
+    // Staging sized to the byte range this worker covers: a quarter of it per
+    // slot once it exceeds kSplitMin, so a mid-sized job still runs as several
+    // groups whose copies, H2Ds and kernels overlap; never below the largest
+    // chunk that fits a slot, and capped at slot_max.
+    constexpr uint64_t kSplitMin = 32ull << 20;
+    uint64_t lo = UINT64_MAX, hi = 0, largest = 0;
     for (uint64_t k = begin; k < end; ++k)
       if ((uint64_t)job.sizes[k] + 15 <= w.slot_max) {
         lo = std::min(lo, job.offsets[k]);
         hi = std::max(hi, job.offsets[k] + job.sizes[k]);
+        largest = std::max<uint64_t>(largest, job.sizes[k]);
       }
+    const uint64_t span = hi > lo ? hi - lo : 0;
+    const uint64_t per = span <= kSplitMin ? span : std::max({kSplitMin, (span + 3) / 4, largest});
     if (end > begin)
-      if (int rc = ensure_slot_bytes(w, std::min(hi > lo ? hi - lo : 0, w.slot_max) + 16)) return rc;
+      if (int rc = ensure_slot_bytes(w, std::min(per, w.slot_max) + 16)) return rc;
   }
   int cur = 0;
   uint64_t i = begin;
@@ -484,7 +495,7 @@ int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
     s.pending = true;
     s.g_begin = i;
     s.g_end = j;
-    cur ^= 1;
+    cur = (cur + 1) % (int)w.slot.size();
     i = j;
   }
   for (Slot& s : w.slot) {

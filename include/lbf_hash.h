@@ -60,7 +60,10 @@ const char* lbf_last_error(void);
 /* Number of visible GPUs (0 when none; never an error on a CPU-only host). */
 int lbf_device_count(int* out_count);
 /* device_mask bit d selects device d; 0 selects every visible device.
- * Fails with LBF_ERR_NO_DEVICE when no GPU is visible. */
+ * Fails with LBF_ERR_NO_DEVICE when no GPU is visible.  Host-path staging,
+ * read at creation: LBF_SLOTS slots per device (2..8, default 3), each grown
+ * on demand up to LBF_SLOT_MB MiB (default 512); LBF_COPY_THREADS host copy
+ * threads (default 8). */
 int lbf_ctx_create(uint32_t device_mask, lbf_ctx** out_ctx);
 void lbf_ctx_destroy(lbf_ctx* ctx);
 int lbf_ctx_num_devices(const lbf_ctx* ctx);

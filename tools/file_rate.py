@@ -61,7 +61,7 @@ def main():
                 t0 = time.perf_counter()
                 d = h.hash_file(path, offs, sizes)
                 rates.append(size / GIB / (time.perf_counter() - t0))
-        # the first full pass grows the pinned staging to 2 x 512 MiB inside the timing
+        # the first full pass grows the pinned staging to 3 x 512 MiB inside the timing
         out["hash_file_first_gibs"] = round(rates[0], 2)
         out["hash_file_steady_gibs"] = [round(r, 2) for r in rates[1:]]
         out["hash_file_parity"] = hashlib.sha1(d.tobytes()).hexdigest() == c2["sha1_of_concat_raw_digests_hex"]
