@@ -137,6 +137,32 @@ def test_small_slots_and_oversize_chunks(variant, oracle):
         h.close()
 
 
+@pytest.mark.parametrize("slots", ["2", "3", "5"])
+def test_staging_slot_counts(slots, oracle):
+    """LBF_SLOTS round-robin staging: a 200 MiB job is split into quarter-span
+    groups (>= 32 MiB each), so every slot is reused; ragged and unaligned
+    chunks straddle the group edges.  Hash and verify both match the oracle."""
+    os.environ["LBF_SLOTS"] = slots
+    try:
+        h = ChunkHasher(device_mask=1)
+    finally:
+        del os.environ["LBF_SLOTS"]
+    try:
+        data = oracle.synth(47, 0, 200 << 20, nthreads=8)
+        offs, sizes = chunk_table(data.size - 5, 262144 + 13)
+        offs = offs + np.uint64(5)
+        want = oracle.sha1_batch(data, offs, sizes, nthreads=8)
+        assert np.array_equal(h.hash_chunks(data, offs, sizes), want)
+        bad = data.copy()
+        flipped = [0, len(sizes) // 2, len(sizes) - 1]
+        for i in flipped:
+            bad[int(offs[i]) + int(sizes[i]) - 1] ^= 0x01
+        v = h.verify_chunks(bad, offs, sizes, want)
+        assert np.nonzero(~v)[0].tolist() == flipped
+    finally:
+        h.close()
+
+
 def test_device_fill_matches_oracle_stream(oracle):
     buf = DeviceBuffer(1 << 20)
     try:
