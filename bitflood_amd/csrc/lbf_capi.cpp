@@ -6,8 +6,9 @@
 // fread -> Base64Encode loop (/root/reference/cpp/src/Encoder.cpp:54-72) and
 // the per-chunk verify loops (Flood.cpp:246-285, ChunkMethods.cpp:111-128,
 // 156-167): the caller hands over a descriptor table, the context copies the
-// covered byte ranges into device slots (double-buffered: host memcpy of group
-// g+1 overlaps H2D + kernel + D2H of group g) and returns digests or verdicts.
+// covered byte ranges into device slots (LBF_SLOTS of them, round-robin: host
+// memcpy of group g+1 overlaps H2D + kernel + D2H of the groups before it) and
+// returns digests or verdicts.
 // Multiple devices take contiguous index ranges, one host thread each, with no
 // collective.
 #include <hip/hip_runtime.h>
@@ -157,7 +158,7 @@ extern "C" int lbf_stream_synchronize(void* s) {
 }
 
 // ---------------------------------------------------------------------------
-// Context: per-device workers with two pipeline slots each.
+// Context: per-device workers with LBF_SLOTS pipeline slots each.
 // ---------------------------------------------------------------------------
 namespace {
 
