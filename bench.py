@@ -9,10 +9,18 @@ shard of an N x 4 GiB file (weak scaling, contiguous chunk ranges, no data-path
 collective; the only collectives are the timing barrier and the max-over-ranks
 reduction).
 
-Launch:  python bench.py [--gpus N --steps K --warmup W]
+--config c4: the C4 shard instead (configs[3]): 32 GiB at 1 MiB chunks per rank,
+rank r = shard r of the 256 GiB file.
+
+Every rank checks its own digests against the committed golden for its shard
+(tests/golden/c2_ranks.json, c4.json) and the pass flags are gathered into the
+line, so a multi-GPU run validates itself.
+
+Launch:  python bench.py [--gpus N --steps K --warmup W] [--config c2|c4]
    N>1:  python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 Rank 0 prints ONE JSON line.
 """
+import math
 import argparse
 import hashlib
 import json
@@ -60,13 +68,19 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--chunk-size", type=int, default=262144)
-    ap.add_argument("--file-gib", type=float, default=4.0, help="bytes hashed per GPU per step")
+    ap.add_argument("--config", choices=["c2", "c4"], default="c2",
+                    help="c2: 4 GiB at 256 KiB per GPU (configs[1]); c4: 32 GiB at 1 MiB per GPU (configs[3])")
+    ap.add_argument("--chunk-size", type=int, default=0, help="override the config's chunk size")
+    ap.add_argument("--file-gib", type=float, default=0.0, help="override the config's bytes per GPU per step")
     ap.add_argument("--variant", type=int, default=0, help="kernel variant (0 = automatic)")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, os.cpu_count())")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="0 = every CPU this process may use (affinity, capped by the cgroup CPU quota)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host->device->host rate")
-    return ap.parse_args()
+    a = ap.parse_args()
+    a.chunk_size = a.chunk_size or {"c2": 262144, "c4": 1 << 20}[a.config]
+    a.file_gib = a.file_gib or {"c2": 4.0, "c4": 32.0}[a.config]
+    return a
 
 
 def dist_setup(args):
@@ -98,42 +112,85 @@ def barrier(world):
         dist.barrier()
 
 
-def traffic_from_profiles(file_bytes, kernel):
+def traffic_from_profiles(file_bytes, chunk_size, kernel):
     """HBM bytes per launch measured with rocprofv3 PMC (FETCH_SIZE x2, gfx950
-    correction), recorded by tools/pmc_traffic.py for this
-    workload size and this kernel."""
+    correction), recorded by tools/pmc_traffic.py --record for
+    this workload size and this kernel.  A static lookup, not a measurement of
+    this run: it goes null when the kernel or the size differ."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(p) as f:
             d = json.load(f)
-        if int(d.get("file_bytes", -1)) == int(file_bytes) and kernel in d.get("kernel", ""):
-            return float(d["hbm_bytes_per_launch"])
+        for e in d.get("entries", [d]):
+            if (int(e.get("file_bytes", -1)) == int(file_bytes) and int(e.get("chunk_size", 262144)) == chunk_size
+                    and kernel in e.get("kernel", "")):
+                return float(e["hbm_bytes_per_launch"]), e.get("source", p)
     except Exception:
         pass
-    return None
+    return None, None
+
+
+def _cgroup_cpu_quota():
+    """CPUs granted by the cgroup v2 quota (cpu.max "quota period"), or None."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        return None if q == "max" else int(q) / int(per)
+    except Exception:
+        return None
+
+
+def _numa_nodes():
+    out = {}
+    base = "/sys/devices/system/node"
+    try:
+        for n in sorted(os.listdir(base)):
+            if n.startswith("node") and n[4:].isdigit():
+                out[n] = open(os.path.join(base, n, "cpulist")).read().strip()
+    except Exception:
+        pass
+    return out
+
+
+def host_cpus():
+    """The CPUs this process can actually use: its affinity mask, capped by the
+    cgroup CPU quota (a GPU box grants 16 CPUs of a 256-CPU host per GPU)."""
+    affinity = len(os.sched_getaffinity(0))
+    quota = _cgroup_cpu_quota()
+    usable = min(affinity, math.ceil(quota)) if quota else affinity
+    return affinity, quota, usable
 
 
 def cpu_baseline(args, stream_start, n_chunks_sample, gpu_digests_sample):
     """The oracle restatement of the reference encoder hash (portable C -O2,
     oracle/sha1_oracle.c) on the host cores, over a bounded sample of the same
     synthetic bytes.  kind="port": building the reference was denied
-    (SURVEY.md §8c)."""
+    (SURVEY.md §8c).  Threads: every CPU the process may use (SURVEY.md §8d
+    (ii)), i.e. its affinity mask capped by the cgroup CPU quota; the same
+    sample on one thread per affinity CPU shows what the quota allows."""
     from tests.oracle_lib import Oracle
     orc = Oracle()
     cs = args.chunk_size
     nbytes = n_chunks_sample * cs
-    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    affinity, quota, usable = host_cpus()
+    threads = args.cpu_threads or usable
     data = orc.synth(SEED_C, stream_start, nbytes, nthreads=threads)
     offs = np.arange(n_chunks_sample, dtype=np.uint64) * np.uint64(cs)
     sizes = np.full(n_chunks_sample, cs, dtype=np.uint32)
-    # all host cores, chunk-parallel (SURVEY.md §8d (ii))
-    reps, t_mt = 0, 0.0
-    while t_mt < 3.0 and reps < 20:
-        t0 = time.perf_counter()
-        d_mt = orc.sha1_batch(data, offs, sizes, nthreads=threads)
-        t_mt += time.perf_counter() - t0
-        reps += 1
-    mt_gibs = reps * nbytes / GIB / t_mt
+
+    def rate(nthreads, min_s=3.0, max_reps=20):
+        reps, t = 0, 0.0
+        d = None
+        while t < min_s and reps < max_reps:
+            t0 = time.perf_counter()
+            d = orc.sha1_batch(data, offs, sizes, nthreads=nthreads)
+            t += time.perf_counter() - t0
+            reps += 1
+        return reps * nbytes / GIB / t, reps, d
+
+    # all usable host cores, chunk-parallel (SURVEY.md §8d (ii))
+    mt_gibs, reps, d_mt = rate(threads)
+    # one thread per CPU of the affinity mask (256 on a GPU box): what the quota lets through
+    aff_gibs = rate(affinity, min_s=1.0, max_reps=3)[0] if affinity != threads else mt_gibs
     # one thread, like Encoder.cpp:40-79 (bounded to 1/4 of the sample)
     n1 = max(1, n_chunks_sample // 4)
     t0 = time.perf_counter()
@@ -146,21 +203,11 @@ def cpu_baseline(args, stream_start, n_chunks_sample, gpu_digests_sample):
         "sample": f"{n_chunks_sample} x {cs // 1024} KiB chunks ({nbytes / GIB:.2f} GiB) of the same stream, "
                   f"{reps} pass(es) on {threads} threads; single-thread pass over {n1} chunks",
         "single_thread_value": round(st_gibs, 3),
-        "host": _host_desc(),
+        "affinity_threads_value": round(aff_gibs, 3),
+        "host": {**_host_desc(), "affinity_cores": affinity, "cgroup_cpu_quota": quota, "usable_cores": usable,
+                 "numa_nodes": _numa_nodes()},
         "parity_vs_gpu": parity,
     }, data
-
-
-def _host_desc():
-    model = ""
-    try:
-        for line in open("/proc/cpuinfo"):
-            if line.startswith("model name"):
-                model = line.split(":", 1)[1].strip()
-                break
-    except Exception:
-        pass
-    return {"cpu_model": model, "os_cpu_count": os.cpu_count()}
 
 
 def compute_floor_ms(variant, cs, n_chunks):
@@ -192,7 +239,46 @@ def e2e_rate(host_data, cs):
         t0 = time.perf_counter()
         d = h.hash_chunks(host_data, offs, sizes)
         t = time.perf_counter() - t0
-    return host_data.size / GIB / t, d
+        placement = h.worker_info(0)
+    return host_data.size / GIB / t, d, placement
+
+
+def golden_for_rank(args, rank, file_bytes):
+    """The committed golden of this rank's shard, or (None, None)."""
+    g = os.path.join(ROOT, "tests", "golden")
+    try:
+        if args.config == "c2" and (file_bytes, args.chunk_size) == (4 * GIB, 262144):
+            d = json.load(open(os.path.join(g, "c2_ranks.json")))
+            return next((r for r in d["ranks"] if r["rank"] == rank), None), "tests/golden/c2_ranks.json"
+        if args.config == "c4" and (file_bytes, args.chunk_size) == (32 * GIB, 1 << 20):
+            d = json.load(open(os.path.join(g, "c4.json")))
+            return next((r for r in d["shards"] if r["rank"] == rank), None), "tests/golden/c4.json"
+    except OSError:
+        pass
+    return None, None
+
+
+def check_golden(gold, digests):
+    """1 = this rank's digests match its golden shard, 0 = mismatch, -1 = no golden."""
+    if gold is None:
+        return -1
+    ok = hashlib.sha1(digests.tobytes()).hexdigest() == gold["sha1_of_concat_raw_digests_hex"]
+    ok = ok and digests.shape[0] == gold["n_chunks"]
+    for k, v in gold.get("samples_b64", {}).items():
+        ok = ok and b64_27(bytes(digests[int(k)])) == v
+    return 1 if ok else 0
+
+
+def gather_ints(x, world):
+    if world == 1:
+        return [int(x)]
+    import torch.distributed as dist
+    backend = dist.get_backend()
+    dev = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
+    t = torch.tensor([int(x)], dtype=torch.int64, device=dev)
+    parts = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(parts, t)
+    return [int(p.item()) for p in parts]
 
 
 def main():
@@ -203,7 +289,7 @@ def main():
     cs = args.chunk_size
     file_bytes = int(args.file_gib * GIB)
     n_chunks = (file_bytes + cs - 1) // cs
-    # this rank's contiguous shard of the N x 4 GiB file (weak scaling)
+    # this rank's contiguous shard of the N x file_bytes file (weak scaling)
     first, last = shard_range(world * n_chunks, rank, world)
     stream_start = first * cs
 
@@ -222,6 +308,7 @@ def main():
     torch.cuda.synchronize()
     barrier(world)
     torch.cuda.synchronize()
+    # HIP events recorded on the stream the kernels run on (torch's current stream)
     e0 = torch.cuda.Event(enable_timing=True)
     e1 = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
@@ -243,10 +330,23 @@ def main():
     achieved_gbs = file_bytes / launch_s / 1e9
 
     digests = dig.download(n_chunks * 20).reshape(n_chunks, 20)
+    # every rank checks its own shard against the committed golden
+    gold, gold_path = golden_for_rank(args, rank, file_bytes)
+    per_rank = gather_ints(check_golden(gold, digests), world)
     variant = H.load().lbf_kernel_for(n_chunks)
     floor_ms = compute_floor_ms(variant, cs, n_chunks)
+    kernel = KERNELS.get(variant, str(variant))
+    traffic, traffic_src = traffic_from_profiles(file_bytes, cs, kernel)
     out = None
     if rank == 0:
+        c2 = (file_bytes, cs) == (4 * GIB, 262144)
+        c4 = (file_bytes, cs) == (32 * GIB, 1 << 20)
+        workload = ("C2 per GPU: one 4 GiB file, 256 KiB chunks, SHA-1 -> 20 B digest per chunk "
+                    "(BASELINE.json configs[1]); N GPUs = N x 4 GiB file, contiguous chunk shards" if c2 else
+                    "C4 per GPU: a 32 GiB shard of the 256 GiB file at 1 MiB chunks, SHA-1 -> 20 B digest per "
+                    "chunk (BASELINE.json configs[3]); rank r hashes shard r" if c4 else
+                    f"custom per GPU: {file_bytes / GIB:g} GiB file, {cs // 1024} KiB chunks, SHA-1 -> 20 B "
+                    f"digest per chunk; N GPUs = N such shards")
         out = {
             "metric": "GiB/s device-resident chunk hashing, 256 KiB chunks, at 1/2/4/8 MI355X",
             "value": round(value, 3),
@@ -262,15 +362,11 @@ def main():
             "data": "synthetic: counter-mode splitmix64 stream seed 0x5EED generated in HBM "
                     f"(rank r hashes bytes [r*{file_bytes / GIB:g}GiB,(r+1)*{file_bytes / GIB:g}GiB) of it)",
             "config": {
-                "workload": "C2 per GPU: one 4 GiB file, 256 KiB chunks, SHA-1 -> 20 B digest per chunk "
-                            "(BASELINE.json configs[1]); N GPUs = N x 4 GiB file, contiguous chunk shards"
-                            if (file_bytes, cs) == (4 * GIB, 262144) else
-                            f"custom per GPU: {file_bytes / GIB:g} GiB file, {cs // 1024} KiB chunks, SHA-1 -> 20 B "
-                            f"digest per chunk; N GPUs = N such shards (C4 per GPU is 32 GiB at 1024 KiB)",
+                "workload": workload,
                 "file_bytes_per_gpu": file_bytes,
                 "chunk_size": cs,
                 "chunks_per_gpu": n_chunks,
-                "kernel": KERNELS.get(variant, str(variant)),
+                "kernel": kernel,
                 "parallelism": f"chunk-shard x{world} (no data-path collective)",
             },
             "roofline": {
@@ -279,9 +375,17 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
-                "traffic": traffic_from_profiles(file_bytes, KERNELS.get(variant, "?")),
+                "traffic": traffic,
+                "traffic_source": traffic_src and f"{traffic_src} (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, same "
+                                                  "kernel and size; a recorded lookup, not this run's counters)",
                 "kernel_ms": round(launch_s * 1e3, 4),
                 "algorithmic_bytes_per_launch": file_bytes,
+                # what the HBM fraction can reach at all: SHA-1 is a serial chain per
+                # chunk, so with this many chunks the launch cannot beat the chain's
+                # instruction-issue floor
+                "ceiling_frac": round(file_bytes / (floor_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                "ceiling_reason": (f"{n_chunks} serial SHA-1 chains: the issue floor below ({floor_ms:.3f} ms) "
+                                   "bounds the launch, not HBM"),
             },
             # SHA-1 is integer VALU work on a serial chain per chunk: the binding
             # limit is instruction issue, not HBM.
@@ -292,19 +396,26 @@ def main():
                 "clock_ghz": CLOCK_HZ / 1e9,
             },
             "digest_check": hashlib.sha1(digests.tobytes()).hexdigest(),
+            "parity": {
+                "golden": gold_path,
+                "per_rank": per_rank,  # 1 match, 0 mismatch, -1 no golden for that shard
+                "all_ranks_match_golden": all(x == 1 for x in per_rank),
+            },
         }
         if world == 1 and not args.no_cpu_baseline:
-            sample = min(n_chunks, 4096)
+            sample = min(n_chunks, max(1, GIB // cs))
             cb, host = cpu_baseline(args, stream_start, sample, digests[:sample])
             out["cpu_baseline"] = cb
             if not args.no_e2e:
-                # the whole C2 file, copied back from HBM into pageable host memory
+                # the whole file, copied back from HBM into pageable host memory
                 host_file = buf.download(file_bytes)
-                rate, d_e2e = e2e_rate(host_file, cs)
+                rate, d_e2e, placement = e2e_rate(host_file, cs)
                 del host_file
                 out["e2e_host_to_host_gibs"] = round(rate, 3)
                 out["e2e_bytes"] = file_bytes
                 out["e2e_parity"] = bool(np.array_equal(d_e2e, digests))
+                out["e2e_staging"] = placement
+                cb["host"]["gpu0_numa_node"] = placement["numa_node"]
         out["first_chunk_b64"] = b64_27(bytes(digests[0]))
     buf.free()
     dig.free()

@@ -21,7 +21,10 @@ except Exception:  # pragma: no cover - torch is part of the image
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _REPO = os.path.dirname(_HERE)
-LIB_PATH = os.path.join(_HERE, "lib", "liblbfhash.so")
+# LBF_LIB: tools only (tools/sweep_variants.py, tools/fuzz_gpu.py) point it at
+# the experimental build (`make -C bitflood_amd/csrc experimental`) that also
+# carries the superseded kernel variants; the product loads the shipped one.
+LIB_PATH = os.environ.get("LBF_LIB") or os.path.join(_HERE, "lib", "liblbfhash.so")
 HEADER_PATH = os.path.join(_REPO, "include", "lbf_hash.h")
 
 LBF_OK = 0
@@ -42,6 +45,9 @@ _SIGS = {
     "lbf_ctx_create": (_c.c_int, [_c.c_uint32, _c.POINTER(_c.c_void_p)]),
     "lbf_ctx_destroy": (None, [_c.c_void_p]),
     "lbf_ctx_num_devices": (_c.c_int, [_c.c_void_p]),
+    "lbf_ctx_num_workers": (_c.c_int, [_c.c_void_p]),
+    "lbf_ctx_worker_info": (_c.c_int, [_c.c_void_p, _c.c_int, _c.POINTER(_c.c_int), _c.POINTER(_c.c_int),
+                                       _c.POINTER(_c.c_int), _c.POINTER(_c.c_int)]),
     "lbf_sha1_batch": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_uint64, _c.c_void_p, _c.c_void_p,
                                   _c.c_uint64, _c.c_void_p, _c.c_int]),
     "lbf_verify_batch": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_uint64, _c.c_void_p, _c.c_void_p,

@@ -102,12 +102,21 @@ __device__ __forceinline__ uint32_t wave_min(uint32_t v) {
 // drains vmcnt(0) before every later ds_read (it cannot tell the staging slots
 // apart), which would collapse the prefetch; here the waits are counted by hand
 // (pc_wait_raw) and the compiler sees no outstanding VMEM op of ours.
+// M0 is declared clobbered.  M0 is a reserved register, so clang warns that
+// the clobber "may not be preserved", but the clobber is what stops the
+// compiler from reusing an M0 value it set before the asm: without it, two
+// __builtin_amdgcn_global_load_lds with the same LDS base around a dma16 share
+// one `s_mov_b32 m0` and the second lands at the dma16's address
+// (tests/c/m0_clobber_probe.hip, pinned by tests/test_isa.py).
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
 __device__ __forceinline__ void dma16(const void* g, uint32_t lds_addr) {
   asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
                :
                : "v"(g), "s"(lds_addr)
-               : "memory");
+               : "memory", "m0");
 }
+#pragma clang diagnostic pop
 
 __device__ __forceinline__ void write_result(const ChunkParams& p, uint32_t i, const Digest& s) {
   uint32_t be[5];

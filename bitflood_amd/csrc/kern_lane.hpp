@@ -1,5 +1,6 @@
-// kern_lane.hpp -- one chunk per lane: "lane" (variant 1), "lds" (3) and
-// "lds2" (11), the kernels for many chains (every SIMD busy).
+// kern_lane.hpp -- one chunk per lane: "lane" (variant 1) and "lds2" (11),
+// the kernels for many chains (every SIMD busy); "lds" (3) only in the
+// LBF_EXPERIMENTAL_VARIANTS build.
 //
 // Part of the single translation unit sha1_kernels.hip (included from there);
 // DESIGN.md §4 has the measurements behind each kernel.
@@ -92,6 +93,7 @@ __global__ void __launch_bounds__(256) sha1_lane_kernel(ChunkParams p) {
 }
 
 
+#ifdef LBF_EXPERIMENTAL_VARIANTS  // not shipped: superseded by lds2 (variant 11)
 // ---------------------------------------------------------------------------
 // Kernel "lds" (variant 3): one chunk per lane for MANY chains.
 //
@@ -163,6 +165,7 @@ __global__ void __launch_bounds__(256) sha1_lds_kernel(ChunkParams p) {
   }
 }
 constexpr int kLdsStages = 2;
+#endif  // LBF_EXPERIMENTAL_VARIANTS
 
 // ---------------------------------------------------------------------------
 // Kernel "lds2" (variant 11): `lds` fetching each chain's bytes a whole 128-B

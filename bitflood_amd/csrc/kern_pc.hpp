@@ -1,6 +1,8 @@
 // kern_pc.hpp -- producer/consumer kernels with one 64-chain pair per
-// workgroup: "pc" (2, and pcx2 = two pairs, 5), "pc2" (4) and "pc4" (6, 7, 8),
-// the kernels for few chains (C2).
+// workgroup, the kernels for few chains (C2): "pc4" reading its schedule as
+// 8-byte pairs (variant 7) is shipped; "pc" (2, and pcx2 = two pairs, 5),
+// "pc2" (4) and the other pc4 layouts (6, 8) are built only with
+// LBF_EXPERIMENTAL_VARIANTS (make experimental), for A/B sweeps.
 //
 // Part of the single translation unit sha1_kernels.hip (included from there);
 // DESIGN.md §4 has the measurements behind each kernel.
@@ -13,6 +15,7 @@
 namespace lbf {
 namespace {
 
+#ifdef LBF_EXPERIMENTAL_VARIANTS  // not shipped: pc (2) and pcx2 (5), superseded by pc4 / pcx5
 // ---------------------------------------------------------------------------
 // Kernel "pc" (variant 2): producer/consumer split for few chains.
 //
@@ -164,6 +167,8 @@ __global__ void __launch_bounds__(128 * kPairs) sha1_pc_kernel(ChunkParams p) {
 #endif
 }
 
+#endif  // LBF_EXPERIMENTAL_VARIANTS
+
 // ---------------------------------------------------------------------------
 // Kernel "pc2" (variant 4): one consumer, TWO producers per 64 chains.
 //
@@ -177,9 +182,11 @@ __global__ void __launch_bounds__(128 * kPairs) sha1_pc_kernel(ChunkParams p) {
 // consumer has passed the barrier that ends its read.  Raw staging: 2 slots of
 // 4 KiB per producer.  LDS 76 KiB -> two workgroups per CU.
 // ---------------------------------------------------------------------------
+constexpr int kP2Raw = 2;  // raw slots per producer (pc2 and pc4)
+#ifdef LBF_EXPERIMENTAL_VARIANTS
 constexpr int kP2Ring = 3;
-constexpr int kP2Raw = 2;  // raw slots per producer
 constexpr int kP2LdsBytes = (kP2Ring * kPcSlotU4 + 2 * kP2Raw * kPcRawU4) * 16;
+#endif
 
 // Raw bytes of `step` into raw slot `slot` of this producer: 4 DMA ops always.
 __device__ __forceinline__ void p2_dma(const ChainInfo& c, uint32_t step, uint32_t raw_lds, uint32_t slot) {
@@ -206,6 +213,7 @@ __device__ __forceinline__ void p2_block(uint32_t (&w)[16], const uint4* raw, co
   }
 }
 
+#ifdef LBF_EXPERIMENTAL_VARIANTS  // not shipped: pc2 (4), superseded by pc4
 template <bool kUniform>
 __global__ void __launch_bounds__(192) sha1_pc2_kernel(ChunkParams p) {
   extern __shared__ __attribute__((aligned(16))) uint4 ring[];  // W[3][20][64] | raw[2][2][4][64]
@@ -294,6 +302,7 @@ __global__ void __launch_bounds__(192) sha1_pc2_kernel(ChunkParams p) {
   }
 #endif
 }
+#endif  // LBF_EXPERIMENTAL_VARIANTS
 
 // ---------------------------------------------------------------------------
 // Kernel "pc4" (variant 6): pc2 with the schedule double-buffered in the
@@ -335,6 +344,7 @@ constexpr int kPc4LdsBytes = (kPc4Ring * kPcSlotU4 + 2 * kP2Raw * kPcRawU4) * 16
 constexpr int kPc4Early = 15;  // loads issued before the first round
 constexpr int kPc4LateAt = 3;  // the rest after quad 3's rounds
 
+#ifdef LBF_EXPERIMENTAL_VARIANTS  // not shipped: the uint4 form of pc4 (variant 6)
 // Step from `cur` (in registers); meanwhile the next step's 20 quads are
 // loaded from `next_slot` (this lane's column) into `nxt`.  Every lane runs
 // the rounds (no divergent branch around the late loads); a lane whose chain
@@ -378,6 +388,7 @@ __device__ __forceinline__ void pc4_compress(Digest& s, const uint4 (&cur)[kPcQu
     s.h[4] = live ? s.h[4] + e : s.h[4];
   }
 }
+#endif  // LBF_EXPERIMENTAL_VARIANTS
 
 // pc4_compress with the schedule read as 40 ds_read_b64 (variant 7).  A lone
 // wave pays ≈96 cycles per block for 20 ds_read_b128 over the same rounds fed
@@ -435,6 +446,7 @@ __device__ __forceinline__ void pc5_compress(Digest& s, const uint2 (&cur)[kPc5P
 // variant 6) or uint2 pairs (kVec 2, variant 7) of the same 20 KiB slot.
 template <int kVec>
 struct Pc4Sched;
+#ifdef LBF_EXPERIMENTAL_VARIANTS
 template <>
 struct Pc4Sched<4> {
   uint4 v[kPcQuads];
@@ -446,6 +458,7 @@ struct Pc4Sched<4> {
     for (int q = 0; q < kPcQuads; ++q) v[q] = src[q * kPcLanes];
   }
 };
+#endif
 template <int kVec>
 struct Pc4Sched {  // kVec 2: uint2 pairs, loads may pair up; kVec 1: single ds_read_b64 each
   uint2 v[kPc5Pairs];
@@ -457,10 +470,12 @@ struct Pc4Sched {  // kVec 2: uint2 pairs, loads may pair up; kVec 1: single ds_
     for (int q = 0; q < kPc5Pairs; ++q) v[q] = src[q * kPcLanes];
   }
 };
+#ifdef LBF_EXPERIMENTAL_VARIANTS
 __device__ __forceinline__ void pc4_step(Digest& s, const Pc4Sched<4>& cur, Pc4Sched<4>& nxt, const uint4* next_slot,
                                          bool live, bool all_live) {
   pc4_compress(s, cur.v, nxt.v, next_slot, live, all_live);
 }
+#endif
 template <int kVec>
 __device__ __forceinline__ void pc4_step(Digest& s, const Pc4Sched<kVec>& cur, Pc4Sched<kVec>& nxt,
                                          const uint2* next_slot, bool live, bool all_live) {

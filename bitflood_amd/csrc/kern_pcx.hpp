@@ -1,5 +1,6 @@
 // kern_pcx.hpp -- two producer/consumer pairs per workgroup pinned to its
-// CU, one producer each: "pcx4" (9) and "pcx5" (10), for 16 K-32 K chains (C4 per GPU).
+// CU, one producer each, for 16 K-32 K chains (C4 per GPU): "pcx5" (10) is
+// shipped, "pcx4" (9) is built only with LBF_EXPERIMENTAL_VARIANTS.
 //
 // Part of the single translation unit sha1_kernels.hip (included from there);
 // DESIGN.md §4 has the measurements behind each kernel.
@@ -46,6 +47,7 @@ __device__ __forceinline__ void px4_round(int i, uint32_t& a, uint32_t& b, uint3
   else round_step_wk(i, a, b, c, d, e, x);
 }
 
+#ifdef LBF_EXPERIMENTAL_VARIANTS  // not shipped: pcx4 (9), superseded by pcx5
 template <int kKFrom>
 __device__ __forceinline__ void px4_compress(Digest& s, const uint2 (&cur)[kPc5Pairs], uint2 (&nxt)[kPc5Pairs],
                                              const uint2* next_slot, const RoundK& K, bool live, bool all_live) {
@@ -196,6 +198,7 @@ void launch_pcx4(const ChunkParams& p, hipStream_t stream) {
   if (p.offsets) hipLaunchKernelGGL((sha1_pcx4_kernel<false, kKFrom>), dim3(blocks), dim3(256), kPx4LdsBytes, stream, p);
   else hipLaunchKernelGGL((sha1_pcx4_kernel<true, kKFrom>), dim3(blocks), dim3(256), kPx4LdsBytes, stream, p);
 }
+#endif  // LBF_EXPERIMENTAL_VARIANTS
 
 // ---------------------------------------------------------------------------
 // Kernel "pcx5" (variant 10): pcx4 with the producer's first 16 words left in

@@ -13,10 +13,15 @@
 // collective.
 #include <hip/hip_runtime.h>
 #include <fcntl.h>
+#include <pthread.h>
+#include <sched.h>
 #include <string.h>
+#include <sys/syscall.h>
 #include <unistd.h>
 
 #include <algorithm>
+#include <cctype>
+#include <cstdio>
 #include <cstdlib>
 #include <mutex>
 #include <string>
@@ -47,6 +52,7 @@ int hip_fail(hipError_t e, const char* what) {
 }  // namespace lbf
 
 using lbf::fail;
+using lbf::hip_fail;
 
 // ---------------------------------------------------------------------------
 // base64-27 (BaseN_Encoder(alphabet, 6), no padding: basecode.cpp:13-37,39-104;
@@ -158,25 +164,144 @@ extern "C" int lbf_stream_synchronize(void* s) {
 }
 
 // ---------------------------------------------------------------------------
-// Context: per-device workers with LBF_SLOTS pipeline slots each.
+// Context: workers (one per device, or LBF_WORKERS_PER_DEVICE per device for
+// tests) with LBF_SLOTS pipeline slots each.
 // ---------------------------------------------------------------------------
 namespace {
 
+uint64_t env_u64(const char* name, uint64_t dflt) {
+  const char* v = getenv(name);
+  if (!v || !*v) return dflt;
+  return strtoull(v, nullptr, 10);
+}
+
+long env_long(const char* name, long dflt) {
+  const char* v = getenv(name);
+  if (!v || !*v) return dflt;
+  return strtol(v, nullptr, 10);
+}
+
+// ---- NUMA placement -----------------------------
+// Each worker's pinned staging is allocated on its GPU's NUMA node and its host
+// threads (the worker thread of a multi-worker job and the staging-copy
+// threads) run on that node's CPUs, so the host memcpy/pread writes local DRAM
+// and the DMA engine reads it without crossing the socket link.  The node comes
+// from the GPU's PCI bus id (/sys/bus/pci/devices/<id>/numa_node); LBF_NUMA=0
+// turns placement off.  Raw syscalls: no libnuma dependency.
+constexpr int kMpolDefault = 0, kMpolPreferred = 1;
+constexpr unsigned long kMpolFNode = 1, kMpolFAddr = 2;
+constexpr unsigned long kMaxNodes = 1024;
+
+bool numa_enabled() {
+  static const bool on = env_long("LBF_NUMA", 1) != 0;
+  return on;
+}
+
+std::string read_line(const std::string& path) {
+  FILE* f = fopen(path.c_str(), "r");
+  if (!f) return "";
+  char buf[4096];
+  std::string out;
+  if (fgets(buf, sizeof(buf), f)) out = buf;
+  fclose(f);
+  while (!out.empty() && (out.back() == '\n' || out.back() == ' ')) out.pop_back();
+  return out;
+}
+
+std::vector<int> parse_cpulist(const std::string& s) {  // "0-63,128-191"
+  std::vector<int> out;
+  size_t p = 0;
+  while (p < s.size()) {
+    char* end = nullptr;
+    const long a = strtol(s.c_str() + p, &end, 10);
+    if (end == s.c_str() + p) break;
+    long b = a;
+    p = (size_t)(end - s.c_str());
+    if (p < s.size() && s[p] == '-') {
+      b = strtol(s.c_str() + p + 1, &end, 10);
+      p = (size_t)(end - s.c_str());
+    }
+    for (long c = a; c <= b && c < CPU_SETSIZE; ++c) out.push_back((int)c);
+    if (p < s.size() && s[p] == ',') ++p;
+    else break;
+  }
+  return out;
+}
+
+int device_numa_node(int device) {
+  char bus[64] = {0};
+  if (hipDeviceGetPCIBusId(bus, sizeof(bus), device) != hipSuccess) return -1;
+  std::string id(bus);
+  for (char& c : id) c = (char)tolower((unsigned char)c);
+  const std::string v = read_line("/sys/bus/pci/devices/" + id + "/numa_node");
+  return v.empty() ? -1 : atoi(v.c_str());
+}
+
+// The node's CPUs that this process may run on (empty: no binding).
+std::vector<int> node_cpus_allowed(int node) {
+  if (node < 0) return {};
+  const std::vector<int> cpus = parse_cpulist(read_line("/sys/devices/system/node/node" + std::to_string(node) + "/cpulist"));
+  cpu_set_t allowed;
+  CPU_ZERO(&allowed);
+  if (sched_getaffinity(0, sizeof(allowed), &allowed) != 0) return {};
+  std::vector<int> out;
+  for (int c : cpus)
+    if (CPU_ISSET(c, &allowed)) out.push_back(c);
+  return out;
+}
+
+void bind_thread(const std::vector<int>& cpus) {
+  if (cpus.empty()) return;
+  cpu_set_t set;
+  CPU_ZERO(&set);
+  for (int c : cpus) CPU_SET(c, &set);
+  (void)pthread_setaffinity_np(pthread_self(), sizeof(set), &set);  // advisory: a refusal only costs locality
+}
+
+// MPOL_PREFERRED(node) for the calling thread while in scope.
+struct PreferNode {
+  bool active = false;
+  int old_mode = kMpolDefault;
+  unsigned long old_mask[kMaxNodes / 64] = {};
+  explicit PreferNode(int node) {
+    if (node < 0 || node >= (int)kMaxNodes) return;
+    if (syscall(SYS_get_mempolicy, &old_mode, old_mask, kMaxNodes, nullptr, 0ul) != 0) return;
+    unsigned long mask[kMaxNodes / 64] = {};
+    mask[node / 64] = 1ul << (node % 64);
+    active = syscall(SYS_set_mempolicy, kMpolPreferred, mask, kMaxNodes) == 0;
+  }
+  ~PreferNode() {
+    if (!active) return;
+    if (old_mode == kMpolDefault) (void)syscall(SYS_set_mempolicy, kMpolDefault, nullptr, 0ul);
+    else (void)syscall(SYS_set_mempolicy, old_mode, old_mask, kMaxNodes);
+  }
+};
+
+// NUMA node of the page holding `p` (-1 when unknown).
+int page_node(const void* p) {
+  if (!p) return -1;
+  int node = -1;
+  if (syscall(SYS_get_mempolicy, &node, nullptr, 0ul, const_cast<void*>(p), kMpolFNode | kMpolFAddr) != 0) return -1;
+  return node;
+}
+
+// ---- workers and slots -----------------------------------------------------
+// A slot's device and pinned buffers are laid out [header | data]: the
+// header holds one group's descriptors (offsets u64[cnt], sizes u32[cnt],
+// expected 20 B x cnt), padded to kHdrAlign, and the chunk bytes follow.  One
+// H2D moves a whole group, one D2H returns its digests or verdicts.
+constexpr uint64_t kHdrAlign = 256;
+constexpr uint64_t kDescBytes = 8 + 4 + 20;
+
+uint64_t header_bytes(uint64_t cnt) { return (cnt * kDescBytes + kHdrAlign - 1) / kHdrAlign * kHdrAlign; }
+
 struct Slot {
   hipStream_t stream = nullptr;
-  uint8_t* d_data = nullptr;       // slot_bytes
-  uint64_t* d_off = nullptr;       // desc_cap
-  uint32_t* d_size = nullptr;
-  uint8_t* d_dig = nullptr;        // desc_cap * 20
-  uint8_t* d_exp = nullptr;
-  uint8_t* d_ver = nullptr;        // desc_cap
-  uint8_t* h_data = nullptr;       // pinned, slot_bytes
-  uint64_t* h_off = nullptr;       // pinned
-  uint32_t* h_size = nullptr;
-  uint8_t* h_dig = nullptr;
-  uint8_t* h_exp = nullptr;
-  uint8_t* h_ver = nullptr;
-  uint8_t* h_ok = nullptr;         // 1 = chunk bytes fully available
+  uint8_t* d_buf = nullptr;  // header | data (hdr_cap + slot_bytes)
+  uint8_t* h_buf = nullptr;  // pinned mirror
+  uint8_t* d_out = nullptr;  // desc_cap * 20: digests, or verdicts
+  uint8_t* h_out = nullptr;  // pinned
+  std::vector<uint8_t> ok;   // 1 = chunk bytes fully available
   // pending group to finalize after the stream drains
   bool pending = false;
   uint64_t g_begin = 0, g_end = 0;
@@ -184,10 +309,15 @@ struct Slot {
 
 struct Worker {
   int device = 0;
-  std::vector<Slot> slot;  // LBF_SLOTS of them (default 3), used round-robin
-  uint64_t slot_bytes = 0;  // current staging capacity per slot (grown on demand)
+  int index = 0;            // position in the context
+  int numa_node = -1;       // the device's NUMA node (-1: unknown / placement off)
+  std::vector<int> cpus;    // CPUs its host threads bind to (empty: unbound)
+  std::vector<Slot> slot;   // LBF_SLOTS of them (default 3), used round-robin
+  uint64_t slot_bytes = 0;  // current data capacity per slot (grown on demand)
   uint64_t slot_max = 0;    // LBF_SLOT_MB: the largest a slot may grow
-  uint64_t desc_cap = 0;
+  uint64_t desc_cap = 0;    // descriptors per group
+  uint64_t hdr_cap = 0;     // header_bytes(desc_cap)
+  long fault_group = -1;    // LBF_TEST_FAULT_GROUP (tests only, one shot)
 };
 
 }  // namespace
@@ -199,10 +329,14 @@ struct lbf_ctx {
 
 namespace {
 
-uint64_t env_u64(const char* name, uint64_t dflt) {
-  const char* v = getenv(name);
-  if (!v || !*v) return dflt;
-  return strtoull(v, nullptr, 10);
+// Pinned host memory on the worker's NUMA node (hipHostMallocNumaUser makes
+// the allocation follow the calling thread's memory policy).
+hipError_t host_alloc(const Worker& w, void** p, uint64_t bytes) {
+  if (w.numa_node >= 0) {
+    PreferNode pref(w.numa_node);
+    if (pref.active) return hipHostMalloc(p, bytes, hipHostMallocNumaUser);
+  }
+  return hipHostMalloc(p, bytes, hipHostMallocDefault);
 }
 
 // Staging memory is sized to the work, not reserved up front: pinning 2 x 512
@@ -216,22 +350,23 @@ int ensure_slot_bytes(Worker& w, uint64_t need) {
   if (need <= w.slot_bytes) return LBF_OK;
   for (Slot& s : w.slot) {
     LBF_HIP_TRY(hipStreamSynchronize(s.stream));
-    if (s.d_data) (void)hipFree(s.d_data);
-    if (s.h_data) (void)hipHostFree(s.h_data);
-    s.d_data = nullptr;
-    s.h_data = nullptr;
+    if (s.d_buf) (void)hipFree(s.d_buf);
+    if (s.h_buf) (void)hipHostFree(s.h_buf);
+    s.d_buf = nullptr;
+    s.h_buf = nullptr;
   }
   w.slot_bytes = 0;
   for (Slot& s : w.slot) {
-    LBF_HIP_TRY(hipMalloc((void**)&s.d_data, need));
-    LBF_HIP_TRY(hipHostMalloc((void**)&s.h_data, need, hipHostMallocDefault));
+    LBF_HIP_TRY(hipMalloc((void**)&s.d_buf, w.hdr_cap + need));
+    LBF_HIP_TRY(host_alloc(w, (void**)&s.h_buf, w.hdr_cap + need));
   }
   w.slot_bytes = need;
   return LBF_OK;
 }
 
-int worker_init(Worker& w, int device) {
+int worker_init(Worker& w, int device, int index) {
   w.device = device;
+  w.index = index;
   w.slot_max = std::max<uint64_t>(env_u64("LBF_SLOT_MB", 512) << 20, 1ull << 20);
   // Three slots keep the PCIe link busy: with two, staging group g+2 waits for
   // group g's H2D *and* its kernel (one chunk's serial chain, ≈3.2 ms at 256 KiB
@@ -239,20 +374,20 @@ int worker_init(Worker& w, int device) {
   w.slot.resize(std::min<uint64_t>(8, std::max<uint64_t>(2, env_u64("LBF_SLOTS", 3))));
   w.slot_bytes = 0;
   w.desc_cap = 1u << 16;
+  w.hdr_cap = header_bytes(w.desc_cap);
+  // Test hook: fail the g-th group this worker stages (once), after earlier
+  // groups are in flight, to exercise the drain on the error path.
+  if (env_long("LBF_TEST_FAULT_WORKER", 0) == index) w.fault_group = env_long("LBF_TEST_FAULT_GROUP", -1);
   LBF_HIP_TRY(hipSetDevice(device));
+  if (numa_enabled()) {
+    w.numa_node = device_numa_node(device);
+    w.cpus = node_cpus_allowed(w.numa_node);
+  }
   for (Slot& s : w.slot) {
     LBF_HIP_TRY(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
-    LBF_HIP_TRY(hipMalloc((void**)&s.d_off, w.desc_cap * 8));
-    LBF_HIP_TRY(hipMalloc((void**)&s.d_size, w.desc_cap * 4));
-    LBF_HIP_TRY(hipMalloc((void**)&s.d_dig, w.desc_cap * 20));
-    LBF_HIP_TRY(hipMalloc((void**)&s.d_exp, w.desc_cap * 20));
-    LBF_HIP_TRY(hipMalloc((void**)&s.d_ver, w.desc_cap));
-    LBF_HIP_TRY(hipHostMalloc((void**)&s.h_off, w.desc_cap * 8, hipHostMallocDefault));
-    LBF_HIP_TRY(hipHostMalloc((void**)&s.h_size, w.desc_cap * 4, hipHostMallocDefault));
-    LBF_HIP_TRY(hipHostMalloc((void**)&s.h_dig, w.desc_cap * 20, hipHostMallocDefault));
-    LBF_HIP_TRY(hipHostMalloc((void**)&s.h_exp, w.desc_cap * 20, hipHostMallocDefault));
-    LBF_HIP_TRY(hipHostMalloc((void**)&s.h_ver, w.desc_cap, hipHostMallocDefault));
-    s.h_ok = new uint8_t[w.desc_cap];
+    LBF_HIP_TRY(hipMalloc((void**)&s.d_out, w.desc_cap * 20));
+    LBF_HIP_TRY(host_alloc(w, (void**)&s.h_out, w.desc_cap * 20));
+    s.ok.assign(w.desc_cap, 0);
   }
   return LBF_OK;
 }
@@ -262,11 +397,10 @@ void worker_free(Worker& w) {
   for (Slot& s : w.slot) {
     // teardown: errors here have nowhere to go, the context is being destroyed
     if (s.stream) (void)hipStreamSynchronize(s.stream);
-    for (void* d : {(void*)s.d_data, (void*)s.d_off, (void*)s.d_size, (void*)s.d_dig, (void*)s.d_exp, (void*)s.d_ver})
-      (void)hipFree(d);
-    for (void* h : {(void*)s.h_data, (void*)s.h_off, (void*)s.h_size, (void*)s.h_dig, (void*)s.h_exp, (void*)s.h_ver})
-      (void)hipHostFree(h);
-    delete[] s.h_ok;
+    if (s.d_buf) (void)hipFree(s.d_buf);
+    if (s.d_out) (void)hipFree(s.d_out);
+    if (s.h_buf) (void)hipHostFree(s.h_buf);
+    if (s.h_out) (void)hipHostFree(s.h_out);
     if (s.stream) (void)hipStreamDestroy(s.stream);
     s = Slot{};
   }
@@ -303,8 +437,9 @@ struct Source {
 
   // A single host thread copies ~17 GiB/s into pinned memory, a third of what
   // PCIe Gen5 moves, so large ranges are split over `threads` contiguous
-  // parts.  Returns the length of the readable prefix, as read_serial does.
-  uint64_t read(uint8_t* dst, uint64_t off, uint64_t len) const {
+  // parts, each on a thread bound to `cpus` (the staging's NUMA node).
+  // Returns the length of the readable prefix, as read_serial does.
+  uint64_t read(uint8_t* dst, uint64_t off, uint64_t len, const std::vector<int>& cpus) const {
     constexpr uint64_t kMinPart = 8ull << 20;
     const uint64_t parts = std::min<uint64_t>(threads, len / kMinPart);
     if (parts <= 1) return read_serial(dst, off, len);
@@ -319,7 +454,10 @@ struct Source {
       const uint64_t a = p * step;
       if (a >= len) break;
       want[p] = std::min(step, len - a);
-      th.emplace_back([&, p, a] { got[p] = read_serial(dst + a, off + a, want[p]); });
+      th.emplace_back([&, p, a] {
+        bind_thread(cpus);
+        got[p] = read_serial(dst + a, off + a, want[p]);
+      });
     }
     for (auto& t : th) t.join();
     uint64_t total = 0;
@@ -347,22 +485,22 @@ int finalize(const Job& job, Slot& s) {
   s.pending = false;
   const uint64_t cnt = s.g_end - s.g_begin;
   if (job.expected) {
-    for (uint64_t k = 0; k < cnt; ++k) job.verdicts[s.g_begin + k] = s.h_ver[k] & s.h_ok[k];
+    for (uint64_t k = 0; k < cnt; ++k) job.verdicts[s.g_begin + k] = s.h_out[k] & s.ok[k];
     return LBF_OK;
   }
   for (uint64_t k = 0; k < cnt; ++k)
-    if (!s.h_ok[k]) return fail(LBF_ERR_IO, "chunk " + std::to_string(s.g_begin + k) + " could not be read in full");
-  memcpy(job.digests + 20 * s.g_begin, s.h_dig, cnt * 20);
+    if (!s.ok[k]) return fail(LBF_ERR_IO, "chunk " + std::to_string(s.g_begin + k) + " could not be read in full");
+  memcpy(job.digests + 20 * s.g_begin, s.h_out, cnt * 20);
   return LBF_OK;
 }
 
-// One chunk that does not fit a slot: a dedicated device buffer.
+// One chunk that does not fit a slot: a dedicated device buffer, synchronous.
 int run_oversize(Worker& w, const Job& job, uint64_t i) {
   Slot& s = w.slot[0];
   LBF_HIP_TRY(hipStreamSynchronize(s.stream));
   const uint32_t sz = job.sizes[i];
   std::vector<uint8_t> host(sz ? sz : 1);
-  const bool ok = job.src.read(host.data(), job.offsets[i], sz) == sz;
+  const bool ok = job.src.read(host.data(), job.offsets[i], sz, w.cpus) == sz;
   if (!ok) {
     if (job.expected) {
       job.verdicts[i] = 0;
@@ -374,37 +512,41 @@ int run_oversize(Worker& w, const Job& job, uint64_t i) {
   LBF_HIP_TRY(hipMalloc((void**)&d, sz ? sz : 1));
   int rc = LBF_OK;
   do {
-    s.h_off[0] = 0;
-    s.h_size[0] = sz;
+    // header of a one-chunk group: offset 0, size sz, expected digest
+    const uint64_t off0 = 0;
+    memcpy(s.h_buf, &off0, 8);
+    memcpy(s.h_buf + 8, &sz, 4);
+    if (job.expected) memcpy(s.h_buf + 12, job.expected + 20 * i, 20);
     if (hipMemcpy(d, host.data(), sz, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(s.d_off, s.h_off, 8, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(s.d_size, s.h_size, 4, hipMemcpyHostToDevice) != hipSuccess) {
+        hipMemcpy(s.d_buf, s.h_buf, kDescBytes, hipMemcpyHostToDevice) != hipSuccess) {
       rc = fail(LBF_ERR_HIP, "oversize chunk H2D failed");
       break;
     }
-    if (job.expected && hipMemcpy(s.d_exp, job.expected + 20 * i, 20, hipMemcpyHostToDevice) != hipSuccess) {
-      rc = fail(LBF_ERR_HIP, "oversize expected H2D failed");
-      break;
-    }
-    rc = lbf_sha1_launch(d, s.d_off, s.d_size, 1, job.expected ? nullptr : s.d_dig,
-                         job.expected ? s.d_exp : nullptr, job.expected ? s.d_ver : nullptr, s.stream);
+    const uint64_t* d_off = reinterpret_cast<const uint64_t*>(s.d_buf);
+    const uint32_t* d_size = reinterpret_cast<const uint32_t*>(s.d_buf + 8);
+    rc = lbf_sha1_launch(d, d_off, d_size, 1, job.expected ? nullptr : s.d_out, job.expected ? s.d_buf + 12 : nullptr,
+                         job.expected ? s.d_out : nullptr, s.stream);
     if (rc) break;
     if (hipStreamSynchronize(s.stream) != hipSuccess) {
       rc = fail(LBF_ERR_HIP, "oversize kernel failed");
       break;
     }
-    const hipError_t e = job.expected ? hipMemcpy(job.verdicts + i, s.d_ver, 1, hipMemcpyDeviceToHost)
-                                      : hipMemcpy(job.digests + 20 * i, s.d_dig, 20, hipMemcpyDeviceToHost);
+    const hipError_t e = job.expected ? hipMemcpy(job.verdicts + i, s.d_out, 1, hipMemcpyDeviceToHost)
+                                      : hipMemcpy(job.digests + 20 * i, s.d_out, 20, hipMemcpyDeviceToHost);
     if (e != hipSuccess) rc = fail(LBF_ERR_HIP, "oversize D2H failed");
   } while (0);
   (void)hipFree(d);
   return rc;
 }
 
-// Process descriptors [begin, end) on one device.  Groups of consecutive
+// Process descriptors [begin, end) on one worker.  Groups of consecutive
 // descriptors whose covering byte range fits a slot are staged into pinned
-// memory (memcpy or pread), then H2D + kernel + D2H run on the slot's stream
-// while the host stages the next group into the other slot.
+// memory (memcpy or pread), then one H2D + kernel + one D2H run on the slot's
+// stream while the host stages the next group into the next slot.
+//
+// Every exit, error or not, passes the drain at the end: each slot's stream is
+// synchronized and its pending group cleared, so nothing is still in flight
+// and no stale group can be finalized into the next job's arrays.
 int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
   LBF_HIP_TRY(hipSetDevice(w.device));
   {
@@ -423,15 +565,21 @@ int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
     const uint64_t span = hi > lo ? hi - lo : 0;
     const uint64_t per = span <= kSplitMin ? span : std::max({kSplitMin, (span + 3) / 4, largest});
     if (end > begin)
-      if (int rc = ensure_slot_bytes(w, std::min(per, w.slot_max) + 16)) return rc;
+      if (int rc = ensure_slot_bytes(w, std::min(per, w.slot_max) + 16)) return rc;  // nothing pending yet
   }
   int cur = 0;
   uint64_t i = begin;
   int rc = LBF_OK;
+  long group = 0;
+  auto hip_ok = [&rc](hipError_t e, const char* what) {
+    if (e == hipSuccess) return true;
+    rc = hip_fail(e, what);
+    return false;
+  };
   while (i < end && rc == LBF_OK) {
     if ((uint64_t)job.sizes[i] + 15 > w.slot_bytes) {
       for (Slot& s : w.slot) {
-        LBF_HIP_TRY(hipStreamSynchronize(s.stream));
+        if (!hip_ok(hipStreamSynchronize(s.stream), "hipStreamSynchronize")) break;
         if ((rc = finalize(job, s))) break;
       }
       if (rc == LBF_OK) rc = run_oversize(w, job, i);
@@ -449,59 +597,55 @@ int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
       ++j;
     }
     Slot& s = w.slot[cur];
-    LBF_HIP_TRY(hipStreamSynchronize(s.stream));
+    if (!hip_ok(hipStreamSynchronize(s.stream), "hipStreamSynchronize")) break;
     if ((rc = finalize(job, s))) break;
+    if (group++ == w.fault_group) {
+      w.fault_group = -1;
+      rc = fail(LBF_ERR_HIP, "injected fault (LBF_TEST_FAULT_GROUP) at group " + std::to_string(group - 1));
+      break;
+    }
     const uint64_t cnt = j - i;
-    // The covered range [lo, hi) lands at h_data + (lo % 16) so each chunk
-    // keeps its offset's 16-byte phase (aligned chunks take the vector-load
-    // path on the device).
+    const uint64_t hdr = header_bytes(cnt);
+    uint64_t* h_off = reinterpret_cast<uint64_t*>(s.h_buf);
+    uint32_t* h_size = reinterpret_cast<uint32_t*>(s.h_buf + 8 * cnt);
+    uint8_t* h_exp = s.h_buf + 12 * cnt;
+    // The covered range [lo, hi) lands at data + (lo % 16) so each chunk keeps
+    // its offset's 16-byte phase (aligned chunks take the vector-load path on
+    // the device).
     const uint64_t shift = lo & 15u;
-    const uint64_t avail = job.src.read(s.h_data + shift, lo, hi - lo);
+    const uint64_t avail = job.src.read(s.h_buf + hdr + shift, lo, hi - lo, w.cpus);
     for (uint64_t k = 0; k < cnt; ++k) {
-      const uint64_t o = job.offsets[i + k];
-      s.h_off[k] = o - lo + shift;
-      s.h_size[k] = job.sizes[i + k];
+      const uint64_t o = job.offsets[i + k], sz = job.sizes[i + k];
       // An empty chunk is always readable, wherever it lies: the reference's
       // fseek succeeds past EOF and fread of 0 bytes returns 0 (Flood.cpp:259-275).
-      s.h_ok[k] = (job.sizes[i + k] == 0 || o + job.sizes[i + k] <= lo + avail) ? 1 : 0;
+      s.ok[k] = (sz == 0 || o + sz <= lo + avail) ? 1 : 0;
+      // Unreadable chunks must not be hashed from stale slot bytes past
+      // `avail`: they get size 0 on the device (their result is discarded).
+      h_off[k] = s.ok[k] ? o - lo + shift : 0;
+      h_size[k] = s.ok[k] ? (uint32_t)sz : 0;
     }
-    const uint64_t copy_bytes = avail + shift;
-    LBF_HIP_TRY(hipMemcpyAsync(s.d_data, s.h_data, copy_bytes, hipMemcpyHostToDevice, s.stream));
-    LBF_HIP_TRY(hipMemcpyAsync(s.d_off, s.h_off, cnt * 8, hipMemcpyHostToDevice, s.stream));
-    LBF_HIP_TRY(hipMemcpyAsync(s.d_size, s.h_size, cnt * 4, hipMemcpyHostToDevice, s.stream));
-    // Unreadable chunks must not be hashed from stale slot bytes past `avail`:
-    // give them size 0 on the device (their result is discarded anyway).
-    bool any_short = false;
-    for (uint64_t k = 0; k < cnt; ++k) any_short |= !s.h_ok[k];
-    if (any_short) {
-      for (uint64_t k = 0; k < cnt; ++k)
-        if (!s.h_ok[k]) {
-          s.h_size[k] = 0;
-          s.h_off[k] = 0;
-        }
-      LBF_HIP_TRY(hipMemcpyAsync(s.d_off, s.h_off, cnt * 8, hipMemcpyHostToDevice, s.stream));
-      LBF_HIP_TRY(hipMemcpyAsync(s.d_size, s.h_size, cnt * 4, hipMemcpyHostToDevice, s.stream));
-    }
-    if (job.expected) {
-      memcpy(s.h_exp, job.expected + 20 * i, cnt * 20);
-      LBF_HIP_TRY(hipMemcpyAsync(s.d_exp, s.h_exp, cnt * 20, hipMemcpyHostToDevice, s.stream));
-      rc = lbf_sha1_launch(s.d_data, s.d_off, s.d_size, cnt, nullptr, s.d_exp, s.d_ver, s.stream);
-      if (rc) break;
-      LBF_HIP_TRY(hipMemcpyAsync(s.h_ver, s.d_ver, cnt, hipMemcpyDeviceToHost, s.stream));
-    } else {
-      rc = lbf_sha1_launch(s.d_data, s.d_off, s.d_size, cnt, s.d_dig, nullptr, nullptr, s.stream);
-      if (rc) break;
-      LBF_HIP_TRY(hipMemcpyAsync(s.h_dig, s.d_dig, cnt * 20, hipMemcpyDeviceToHost, s.stream));
-    }
+    if (job.expected) memcpy(h_exp, job.expected + 20 * i, cnt * 20);
+    if (!hip_ok(hipMemcpyAsync(s.d_buf, s.h_buf, hdr + shift + avail, hipMemcpyHostToDevice, s.stream),
+                "hipMemcpyAsync(H2D)"))
+      break;
+    const uint64_t* d_off = reinterpret_cast<const uint64_t*>(s.d_buf);
+    const uint32_t* d_size = reinterpret_cast<const uint32_t*>(s.d_buf + 8 * cnt);
+    if (job.expected) rc = lbf_sha1_launch(s.d_buf + hdr, d_off, d_size, cnt, nullptr, s.d_buf + 12 * cnt, s.d_out, s.stream);
+    else rc = lbf_sha1_launch(s.d_buf + hdr, d_off, d_size, cnt, s.d_out, nullptr, nullptr, s.stream);
+    if (rc) break;
+    if (!hip_ok(hipMemcpyAsync(s.h_out, s.d_out, cnt * (job.expected ? 1 : 20), hipMemcpyDeviceToHost, s.stream),
+                "hipMemcpyAsync(D2H)"))
+      break;
     s.pending = true;
     s.g_begin = i;
     s.g_end = j;
     cur = (cur + 1) % (int)w.slot.size();
     i = j;
   }
+  // drain, on every path
   for (Slot& s : w.slot) {
-    if (hipStreamSynchronize(s.stream) != hipSuccess && rc == LBF_OK)
-      rc = fail(LBF_ERR_HIP, "stream synchronize failed");
+    const hipError_t e = hipStreamSynchronize(s.stream);
+    if (e != hipSuccess && rc == LBF_OK) rc = hip_fail(e, "hipStreamSynchronize");
     if (rc == LBF_OK) rc = finalize(job, s);
     s.pending = false;
   }
@@ -517,6 +661,8 @@ int validate_memory_job(const Job& job, uint64_t n) {
   return LBF_OK;
 }
 
+// Contiguous index ranges per worker, one host thread each (bound to its
+// worker's NUMA node), no collective.
 int run_job(lbf_ctx* ctx, const Job& job, uint64_t n) {
   std::lock_guard<std::mutex> lock(ctx->mu);
   const size_t nw = ctx->workers.size();
@@ -527,13 +673,16 @@ int run_job(lbf_ctx* ctx, const Job& job, uint64_t n) {
   for (size_t d = 0; d < nw; ++d) {
     const uint64_t b = n * d / nw, e = n * (d + 1) / nw;
     th.emplace_back([&, d, b, e] {
+      bind_thread(ctx->workers[d].cpus);
       rcs[d] = worker_run(ctx->workers[d], job, b, e);
       if (rcs[d]) errs[d] = lbf_last_error();
     });
   }
   for (auto& t : th) t.join();
   for (size_t d = 0; d < nw; ++d)
-    if (rcs[d]) return fail(rcs[d], "device " + std::to_string(ctx->workers[d].device) + ": " + errs[d]);
+    if (rcs[d])
+      return fail(rcs[d], "worker " + std::to_string(d) + " (device " + std::to_string(ctx->workers[d].device) +
+                              "): " + errs[d]);
   return LBF_OK;
 }
 
@@ -562,14 +711,20 @@ extern "C" int lbf_ctx_create(uint32_t device_mask, lbf_ctx** out) {
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
     return fail(LBF_ERR_NO_DEVICE, "no GPU visible: the chunk-hash path runs only on MI355X (no CPU fallback)");
+  // Test knob: k workers per selected device, so the multi-worker split, the
+  // per-worker staging and the error propagation of run_job run on a one-GPU
+  // box exactly as they do with one worker per GPU on an 8-GPU node.
+  const int per_dev = (int)std::max(1L, std::min(16L, env_long("LBF_WORKERS_PER_DEVICE", 1)));
   lbf_ctx* ctx = new lbf_ctx();
   for (int d = 0; d < ndev && d < 32; ++d) {
     if (device_mask && !(device_mask & (1u << d))) continue;
-    ctx->workers.emplace_back();
-    if (int rc = worker_init(ctx->workers.back(), d)) {
-      std::string msg = lbf_last_error();
-      lbf_ctx_destroy(ctx);
-      return fail(rc, msg);
+    for (int k = 0; k < per_dev; ++k) {
+      ctx->workers.emplace_back();
+      if (int rc = worker_init(ctx->workers.back(), d, (int)ctx->workers.size() - 1)) {
+        std::string msg = lbf_last_error();
+        lbf_ctx_destroy(ctx);
+        return fail(rc, msg);
+      }
     }
   }
   if (ctx->workers.empty()) {
@@ -580,13 +735,31 @@ extern "C" int lbf_ctx_create(uint32_t device_mask, lbf_ctx** out) {
   return LBF_OK;
 }
 
+extern "C" int lbf_ctx_worker_info(const lbf_ctx* ctx, int worker, int* device, int* numa_node, int* staging_node,
+                                   int* bound_cpus) {
+  if (!ctx || worker < 0 || worker >= (int)ctx->workers.size()) return fail(LBF_ERR_INVALID, "no such worker");
+  const Worker& w = ctx->workers[worker];
+  if (device) *device = w.device;
+  if (numa_node) *numa_node = w.numa_node;
+  if (staging_node) *staging_node = page_node(w.slot.empty() ? nullptr : (w.slot[0].h_buf ? w.slot[0].h_buf : w.slot[0].h_out));
+  if (bound_cpus) *bound_cpus = (int)w.cpus.size();
+  return LBF_OK;
+}
+
 extern "C" void lbf_ctx_destroy(lbf_ctx* ctx) {
   if (!ctx) return;
   for (Worker& w : ctx->workers) worker_free(w);
   delete ctx;
 }
 
-extern "C" int lbf_ctx_num_devices(const lbf_ctx* ctx) { return ctx ? (int)ctx->workers.size() : 0; }
+extern "C" int lbf_ctx_num_devices(const lbf_ctx* ctx) {
+  if (!ctx) return 0;
+  int n = 0;
+  for (size_t k = 0; k < ctx->workers.size(); ++k) n += (k == 0 || ctx->workers[k].device != ctx->workers[k - 1].device);
+  return n;
+}
+
+extern "C" int lbf_ctx_num_workers(const lbf_ctx* ctx) { return ctx ? (int)ctx->workers.size() : 0; }
 
 extern "C" int lbf_sha1_batch(lbf_ctx* ctx, const uint8_t* base, uint64_t base_len, const uint64_t* offsets,
                               const uint32_t* sizes, uint64_t n, uint8_t* out_digests, int flags) {

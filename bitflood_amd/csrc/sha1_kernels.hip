@@ -5,20 +5,21 @@
 // verify hashes of Flood.cpp:259-275 / ChunkMethods.cpp:116-123,165-167 with
 // one batched launch over many independent chunks.
 //
-// Kernel "lane" (variant 1): one chunk per lane.  SHA-1 is a serial
-// Merkle-Damgard chain, so the only parallelism is across chunks; each lane
-// keeps its chain state and the 16-word schedule in VGPRs, streams its chunk
-// with 16-byte global loads two blocks ahead of use, and finishes the 0x80/
-// length padding in registers.  See DESIGN.md for the roofline discussion.
-// Kernel "pc" (variant 2): producer/consumer split for few chains.
-// Kernel "lds" (variant 3): variant 1 with LDS-DMA staging, for many chains.
-// Kernel "pc2" (variant 4): one consumer + two producers, W+K hand-over, for few chains.
-// Kernel "pcx2" (variant 5): two pc pairs in one workgroup pinned to its CU, for 16-32 K chains.
-// Kernel "pc4" (variant 6): pc2 with the schedule double-buffered in registers, for <= 16 K chains.
-// Kernel "pc4/b64" (variants 7, 8): pc4 with the schedule read as uint2 pairs (8: one ds_read_b64 each).
-// Kernel "pcx4" (variant 9): two pc4-style pairs per CU, one producer each, K split, for 16-32 K chains.
-// Kernel "pcx5" (variant 10): pcx4 with words 0..15 taken by the consumer from the raw block, for 16-32 K chains.
-// Kernel "lds2" (variant 11): lds fetching whole 128-byte lines per lane, for > 32 K chains.
+// Shipped kernels (lbf_kernel_for picks one by chain count):
+//   "lane" (variant 1): one chunk per lane, the simple baseline.  SHA-1 is a
+//     serial Merkle-Damgard chain, so the only parallelism is across chunks;
+//     each lane keeps its chain state and the 16-word schedule in VGPRs.
+//   "pc4/b64" (variant 7): one consumer + two producer waves per 64 chains, the
+//     W+K schedule handed over in LDS and double-buffered in the consumer's
+//     registers as 8-byte pairs -- few chains (<= 16 K, C2).
+//   "pcx5" (variant 10): two consumer/producer pairs per CU, K split between
+//     them, words 0..15 read by the consumer from the raw block -- 16-32 K
+//     chains (C4 per GPU).
+//   "lds2" (variant 11): one chunk per lane with LDS-DMA staging of whole
+//     128-byte lines -- many chains (C3).
+// The superseded variants (2 pc, 3 lds, 4 pc2, 5 pcx2, 6 pc4/uint4, 8 pc4/b64
+// single loads, 9 pcx4) are compiled only with -DLBF_EXPERIMENTAL_VARIANTS
+// (`make experimental`), for A/B sweeps (tools/sweep_variants.py).
 #include <hip/hip_runtime.h>
 
 #include <atomic>
@@ -94,9 +95,53 @@ int pick_variant(uint64_t n) {
   return variant;
 }
 
-int launch_chunks(const ChunkParams& p, hipStream_t stream) {
-  if (p.n == 0) return LBF_OK;
-  const int variant = pick_variant(p.n);
+template <bool kUniform>
+void launch_pc4(const ChunkParams& p, hipStream_t stream, int kvec) {
+  static std::once_flag once;
+  std::call_once(once, [] {
+    for (const void* f : {reinterpret_cast<const void*>(&sha1_pc4_kernel<kUniform, 2>),
+#ifdef LBF_EXPERIMENTAL_VARIANTS
+                          reinterpret_cast<const void*>(&sha1_pc4_kernel<kUniform, 4>),
+                          reinterpret_cast<const void*>(&sha1_pc4_kernel<kUniform, 1>),
+#endif
+                         })
+      hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kPc4LdsBytes);
+  });
+  const dim3 g((p.n + kPcLanes - 1) / kPcLanes), b(192);
+#ifdef LBF_EXPERIMENTAL_VARIANTS
+  if (kvec == 4) {
+    hipLaunchKernelGGL((sha1_pc4_kernel<kUniform, 4>), g, b, kPc4LdsBytes, stream, p);
+    return;
+  }
+  if (kvec == 1) {
+    hipLaunchKernelGGL((sha1_pc4_kernel<kUniform, 1>), g, b, kPc4LdsBytes, stream, p);
+    return;
+  }
+#endif
+  (void)kvec;
+  hipLaunchKernelGGL((sha1_pc4_kernel<kUniform, 2>), g, b, kPc4LdsBytes, stream, p);
+}
+
+template <bool kUniform>
+void launch_lds2(const ChunkParams& p, hipStream_t stream) {
+  static std::once_flag once;
+  std::call_once(once, [] {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_lds2_kernel<kUniform>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, kLds2Bytes);
+  });
+  hipLaunchKernelGGL(sha1_lds2_kernel<kUniform>, dim3((p.n + 255) / 256), dim3(256), kLds2Bytes, stream, p);
+}
+
+template <bool kUniform>
+void launch_lane(const ChunkParams& p, hipStream_t stream) {
+  // 64-thread workgroups while waves are scarce so they spread over every CU.
+  const uint32_t threads = p.n <= 65536u ? 64u : 256u;
+  hipLaunchKernelGGL(sha1_lane_kernel<kUniform>, dim3((p.n + threads - 1) / threads), dim3(threads), 0, stream, p);
+}
+
+#ifdef LBF_EXPERIMENTAL_VARIANTS
+// Superseded variants, kept for A/B sweeps: false when `variant` is not one.
+bool launch_experimental(int variant, const ChunkParams& p, hipStream_t stream) {
   if (variant == 2) {
     const uint32_t blocks = (p.n + kPcLanes - 1) / kPcLanes;
     constexpr int lds = pc_lds_bytes<2>();
@@ -125,58 +170,45 @@ int launch_chunks(const ChunkParams& p, hipStream_t stream) {
     const uint32_t blocks = (p.n + kPcLanes - 1) / kPcLanes;
     if (p.offsets) hipLaunchKernelGGL(sha1_pc2_kernel<false>, dim3(blocks), dim3(192), kP2LdsBytes, stream, p);
     else hipLaunchKernelGGL(sha1_pc2_kernel<true>, dim3(blocks), dim3(192), kP2LdsBytes, stream, p);
-  } else if (variant == 6 || variant == 7 || variant == 8) {
-    static std::once_flag once;
-    std::call_once(once, [] {
-      for (const void* f : {reinterpret_cast<const void*>(&sha1_pc4_kernel<false, 4>),
-                            reinterpret_cast<const void*>(&sha1_pc4_kernel<true, 4>),
-                            reinterpret_cast<const void*>(&sha1_pc4_kernel<false, 2>),
-                            reinterpret_cast<const void*>(&sha1_pc4_kernel<true, 2>),
-                            reinterpret_cast<const void*>(&sha1_pc4_kernel<false, 1>),
-                            reinterpret_cast<const void*>(&sha1_pc4_kernel<true, 1>)})
-        hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kPc4LdsBytes);
-    });
-    const uint32_t blocks = (p.n + kPcLanes - 1) / kPcLanes;
-    const dim3 g(blocks), b(192);
-    if (variant == 6) {
-      if (p.offsets) hipLaunchKernelGGL((sha1_pc4_kernel<false, 4>), g, b, kPc4LdsBytes, stream, p);
-      else hipLaunchKernelGGL((sha1_pc4_kernel<true, 4>), g, b, kPc4LdsBytes, stream, p);
-    } else if (variant == 7) {
-      if (p.offsets) hipLaunchKernelGGL((sha1_pc4_kernel<false, 2>), g, b, kPc4LdsBytes, stream, p);
-      else hipLaunchKernelGGL((sha1_pc4_kernel<true, 2>), g, b, kPc4LdsBytes, stream, p);
-    } else {
-      if (p.offsets) hipLaunchKernelGGL((sha1_pc4_kernel<false, 1>), g, b, kPc4LdsBytes, stream, p);
-      else hipLaunchKernelGGL((sha1_pc4_kernel<true, 1>), g, b, kPc4LdsBytes, stream, p);
-    }
+  } else if (variant == 6 || variant == 8) {
+    const int kvec = variant == 6 ? 4 : 1;
+    if (p.offsets) launch_pc4<false>(p, stream, kvec);
+    else launch_pc4<true>(p, stream, kvec);
   } else if (variant == 9) {
     launch_pcx4<kPx4KFrom>(p, stream);
-  } else if (variant == 10) {
-    launch_pcx5<kPx5KFrom>(p, stream);
-  } else if (variant == 11) {
-    static std::once_flag once;
-    std::call_once(once, [] {
-      hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_lds2_kernel<false>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, kLds2Bytes);
-      hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_lds2_kernel<true>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, kLds2Bytes);
-    });
-    const uint32_t blocks = (p.n + 255) / 256;
-    if (p.offsets) hipLaunchKernelGGL(sha1_lds2_kernel<false>, dim3(blocks), dim3(256), kLds2Bytes, stream, p);
-    else hipLaunchKernelGGL(sha1_lds2_kernel<true>, dim3(blocks), dim3(256), kLds2Bytes, stream, p);
   } else if (variant == 3) {
     const uint32_t blocks = (p.n + 255) / 256;
     constexpr int lds = 4 * kLdsStages * kPcRawU4 * 16;
     if (p.offsets) hipLaunchKernelGGL((sha1_lds_kernel<false, kLdsStages>), dim3(blocks), dim3(256), lds, stream, p);
     else hipLaunchKernelGGL((sha1_lds_kernel<true, kLdsStages>), dim3(blocks), dim3(256), lds, stream, p);
   } else {
-    // 64-thread workgroups while waves are scarce so they spread over every CU.
-    const uint32_t threads = p.n <= 65536u ? 64u : 256u;
-    const uint32_t blocks = (p.n + threads - 1) / threads;
-    if (p.offsets) {
-      hipLaunchKernelGGL(sha1_lane_kernel<false>, dim3(blocks), dim3(threads), 0, stream, p);
-    } else {
-      hipLaunchKernelGGL(sha1_lane_kernel<true>, dim3(blocks), dim3(threads), 0, stream, p);
-    }
+    return false;
+  }
+  return true;
+}
+#endif
+
+int launch_chunks(const ChunkParams& p, hipStream_t stream) {
+  if (p.n == 0) return LBF_OK;
+  const int variant = pick_variant(p.n);
+  const bool uniform = p.offsets == nullptr;
+#ifdef LBF_EXPERIMENTAL_VARIANTS
+  if (launch_experimental(variant, p, stream)) {
+    LBF_HIP_TRY(hipGetLastError());
+    return LBF_OK;
+  }
+#endif
+  if (variant == 7) {
+    if (uniform) launch_pc4<true>(p, stream, 2);
+    else launch_pc4<false>(p, stream, 2);
+  } else if (variant == 10) {
+    launch_pcx5<kPx5KFrom>(p, stream);
+  } else if (variant == 11) {
+    if (uniform) launch_lds2<true>(p, stream);
+    else launch_lds2<false>(p, stream);
+  } else {
+    if (uniform) launch_lane<true>(p, stream);
+    else launch_lane<false>(p, stream);
   }
   LBF_HIP_TRY(hipGetLastError());
   return LBF_OK;
@@ -239,7 +271,12 @@ extern "C" int lbf_sha1_uniform_launch(const uint8_t* d_base, uint64_t len, uint
 }
 
 extern "C" int lbf_set_kernel_variant(int variant) {
-  if (variant < 0 || variant > 11) return fail(LBF_ERR_INVALID, "unknown kernel variant");
+#ifdef LBF_EXPERIMENTAL_VARIANTS
+  const bool known = variant >= 0 && variant <= 11;
+#else
+  const bool known = variant == 0 || variant == 1 || variant == 7 || variant == 10 || variant == 11;
+#endif
+  if (!known) return fail(LBF_ERR_INVALID, "unknown kernel variant (shipped: 0 auto, 1, 7, 10, 11)");
   lbf::g_variant.store(variant);
   return LBF_OK;
 }

@@ -25,6 +25,10 @@ from . import _capi
 from ._capi import LBF_DEVICE_PTR, LBF_HOST_PTR, LbfError, check, load
 
 DIGEST = 20
+# A valid one-byte host buffer that lives as long as the process: the base
+# pointer for batches over empty data (every chunk then has size 0, so nothing
+# is read from it, but the library still gets a real address).
+_EMPTY = (ctypes.c_uint8 * 1)()
 
 
 def b64_27(digest: bytes) -> str:
@@ -76,6 +80,17 @@ class ChunkHasher:
     def num_devices(self) -> int:
         return self._lib.lbf_ctx_num_devices(self._h)
 
+    @property
+    def num_workers(self) -> int:
+        return self._lib.lbf_ctx_num_workers(self._h)
+
+    def worker_info(self, worker: int = 0) -> dict:
+        """Device, its NUMA node, the node of the worker's pinned staging and the
+        number of CPUs its host threads are bound to (see lbf_ctx_worker_info)."""
+        v = [ctypes.c_int(-9) for _ in range(4)]
+        check(self._lib.lbf_ctx_worker_info(self._h, worker, *[ctypes.byref(x) for x in v]))
+        return dict(zip(["device", "numa_node", "staging_node", "bound_cpus"], [x.value for x in v]))
+
     def close(self) -> None:
         if self._h:
             self._lib.lbf_ctx_destroy(self._h)
@@ -104,7 +119,7 @@ class ChunkHasher:
         out = np.zeros((n, DIGEST), dtype=np.uint8)
         if n == 0:
             return out
-        base = buf.ctypes.data if buf.size else ctypes.addressof(ctypes.c_uint8(0))
+        base = buf.ctypes.data if buf.size else ctypes.addressof(_EMPTY)
         check(self._lib.lbf_sha1_batch(self._h, base, buf.size, offs.ctypes.data, szs.ctypes.data, n,
                                        out.ctypes.data, LBF_HOST_PTR))
         return out
@@ -120,7 +135,7 @@ class ChunkHasher:
         ver = np.zeros(n, dtype=np.uint8)
         if n == 0:
             return ver.astype(bool)
-        base = buf.ctypes.data if buf.size else ctypes.addressof(ctypes.c_uint8(0))
+        base = buf.ctypes.data if buf.size else ctypes.addressof(_EMPTY)
         check(self._lib.lbf_verify_batch(self._h, base, buf.size, offs.ctypes.data, szs.ctypes.data, n,
                                          exp.ctypes.data, ver.ctypes.data, LBF_HOST_PTR))
         return ver.astype(bool)
@@ -157,7 +172,7 @@ class ChunkHasher:
     def sha1(self, data) -> bytes:
         buf = _as_u8(data)
         out = (ctypes.c_uint8 * DIGEST)()
-        base = buf.ctypes.data if buf.size else None
+        base = buf.ctypes.data if buf.size else ctypes.addressof(_EMPTY)
         check(self._lib.lbf_sha1_one(self._h, base, buf.size, out))
         return bytes(out)
 

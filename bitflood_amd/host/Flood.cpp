@@ -263,10 +263,10 @@ Error::ErrorCode Flood::ReadVerifiedChunks(const std::vector<P_ChunkKey>& i_keys
   return Error::NO_ERROR_LBF;
 }
 
-Error::ErrorCode Flood::ReceiveChunks(const U8* i_arena, U64 i_arena_len, const std::vector<ChunkArrival>& i_chunks,
-                                      std::string& o_accepted) {
+Error::ErrorCode Flood::VerifyChunks(const U8* i_arena, U64 i_arena_len, const std::vector<ChunkArrival>& i_chunks,
+                                     std::string& o_valid) {
   const size_t n = i_chunks.size();
-  o_accepted.assign(n, '0');
+  o_valid.assign(n, '0');
   std::vector<U64> voff;
   std::vector<U32> vsz;
   std::vector<U8> vexp;
@@ -293,15 +293,30 @@ Error::ErrorCode Flood::ReceiveChunks(const U8* i_arena, U64 i_arena_len, const 
   if (lbf_verify_batch(ctx, i_arena_len ? i_arena : &kEmpty, i_arena_len, &voff[0], &vsz[0], which.size(), &vexp[0],
                        &verdict[0], LBF_HOST_PTR) != LBF_OK)
     return Error::UNKNOWN_ERROR_LBF;
+  for (size_t j = 0; j < which.size(); ++j)
+    if (verdict[j]) o_valid[which[j]] = '1';
+  return Error::NO_ERROR_LBF;
+}
+
+Error::ErrorCode Flood::ReceiveChunks(const U8* i_arena, U64 i_arena_len, const std::vector<ChunkArrival>& i_chunks,
+                                      std::string& o_accepted) {
+  const size_t n = i_chunks.size();
+  o_accepted.assign(n, '0');
+  std::string valid;
+  const Error::ErrorCode rc = VerifyChunks(i_arena, i_arena_len, i_chunks, valid);
+  if (rc != Error::NO_ERROR_LBF) return rc;
+  std::vector<size_t> which;
+  for (size_t k = 0; k < n; ++k)
+    if (valid[k] == '1') which.push_back(k);
+  if (which.empty()) return Error::NO_ERROR_LBF;
   // write the accepted chunks: one open per file (fopen "r+b" else "w+b", :169-173)
   std::map<std::string, int> fds;
-  for (size_t j = 0; j < which.size(); ++j) {
-    const std::string& name = i_chunks[which[j]].m_filename;
-    if (verdict[j] && !fds.count(name)) fds[name] = open(PathOf(name).c_str(), O_RDWR | O_CREAT, 0644);
+  for (size_t k : which) {
+    const std::string& name = i_chunks[k].m_filename;
+    if (!fds.count(name)) fds[name] = open(PathOf(name).c_str(), O_RDWR | O_CREAT, 0644);
   }
   std::vector<U8> written(which.size(), 0);
   parallel_for(which.size(), io_threads(), [&](size_t j) {
-    if (!verdict[j]) return;  // bad chunk silently dropped (:167)
     const ChunkArrival& a = i_chunks[which[j]];
     const int fd = fds.find(a.m_filename)->second;
     if (fd < 0) return;

@@ -104,12 +104,20 @@ bool parse_value(const char* s, size_t len, size_t& off, Value& v, U8* dst, size
   const std::string tag = get_next_tag(s, len, off);
   bool ok = false;
   if (tag == "<i4>" || tag == "<int>") {
+    // intFromXml is strtol on the rest of the buffer; the frame is (ptr, len)
+    // and need not be NUL-terminated, so strtol runs on a bounded copy.  63
+    // chars hold any whitespace + sign + digits strtol would still accept
+    // without saturating differently.
+    char tok[64];
+    const size_t n = std::min(sizeof(tok) - 1, len - off);
+    memcpy(tok, s + off, n);
+    tok[n] = '\0';
     char* end = nullptr;
-    const long x = strtol(s + off, &end, 10);  // intFromXml
-    if (end != s + off) {
+    const long x = strtol(tok, &end, 10);
+    if (end != tok) {
       v.m_type = Value::INT;
       v.m_int = (int)x;
-      off = (size_t)(end - s);
+      off += (size_t)(end - tok);
       ok = next_tag_is(tag == "<i4>" ? "</i4>" : "</int>", s, len, off);
     }
   } else if (tag.empty() || tag == "<string>" || tag == "</value>") {

@@ -20,6 +20,13 @@
 //    and up to --batch requests per launch on the seeder (ReadVerifiedChunks).
 // With --corrupt K the seeder flips one byte of every K-th chunk AFTER its own
 // verify (a wire error); the leecher must reject it and ask again.
+// With --synthetic the seeder holds no file: its chunk bytes come from the
+// counter-mode generator (the stream lbf_fill_synthetic writes), re-verified on
+// the GPU against the flood file before sending (Flood::VerifyChunks, the verify
+// half of _HandleRequestChunk), and the flood file is encoded from the same
+// stream generated in HBM.  Only the leecher's copy touches the disk, so the
+// 16 GiB C5 transfer needs 16 GiB of scratch space, not 32; the written file is
+// compared with the generator instead of a source file.
 //
 // Prints one JSON line: payload rate, verify latency, batch sizes, and the end
 // state (resume verify of the written file, byte comparison with the source).
@@ -65,6 +72,7 @@ struct Opts {
   U32 corrupt = 0;
   std::string dir;
   bool keep = false;
+  bool synthetic = false;
 };
 
 [[noreturn]] void die(const std::string& m) {
@@ -191,6 +199,80 @@ void write_source(const std::string& path, U64 size, unsigned threads) {
   if (!ok) die("writing " + path + " failed");
 }
 
+constexpr U64 kSeed = 0xC5;
+
+// Bytes [off, off + len) of the synthetic stream.
+void synth_bytes(U8* dst, U64 off, U64 len) {
+  U64 k = off / 8, pos = off;
+  const U64 end = off + len;
+  if (pos % 8) {  // leading partial word
+    const U64 w = synth_word(kSeed, k++);
+    for (; pos < end && pos % 8; ++pos) *dst++ = (U8)(w >> (8 * (pos % 8)));
+  }
+  for (; pos + 8 <= end; pos += 8, dst += 8) {
+    const U64 w = synth_word(kSeed, k++);
+    memcpy(dst, &w, 8);
+  }
+  if (pos < end) {
+    const U64 w = synth_word(kSeed, k);
+    for (U64 b = 0; pos < end; ++pos, ++b) *dst++ = (U8)(w >> (8 * b));
+  }
+}
+
+// The flood file of the synthetic stream, hashed where it is generated: in HBM
+// (lbf_fill_synthetic + one device-resident batch launch), like test_encoder
+// run over the seeder's file.
+void encode_synthetic(const std::string& name, U64 size, U32 cs, FloodFile& ff) {
+  const U64 n = (size + cs - 1) / cs;
+  FloodFile::FileSPtr file(new FloodFile::File());
+  file->m_name = name;
+  file->m_size = size;
+  file->m_chunks.resize(n);
+  if (n) {
+    void *d_buf = nullptr, *d_dig = nullptr;
+    if (lbf_dev_malloc(&d_buf, size) != LBF_OK || lbf_dev_malloc(&d_dig, n * 20) != LBF_OK ||
+        lbf_fill_synthetic((U8*)d_buf, size, kSeed, 0, nullptr) != LBF_OK ||
+        lbf_sha1_uniform_launch((const U8*)d_buf, size, cs, 0, n, (U8*)d_dig, nullptr, nullptr, nullptr) != LBF_OK ||
+        lbf_device_synchronize() != LBF_OK)
+      die(std::string("synthetic encode failed: ") + lbf_last_error());
+    V_U8 dig(n * 20);
+    if (lbf_memcpy_d2h(dig.data(), d_dig, n * 20) != LBF_OK) die(std::string("D2H failed: ") + lbf_last_error());
+    lbf_dev_free(d_buf);
+    lbf_dev_free(d_dig);
+    for (U64 i = 0; i < n; ++i) {
+      FloodFile::Chunk& c = file->m_chunks[i];
+      c.m_index = (U32)i;
+      c.m_size = (U32)std::min<U64>(cs, size - i * cs);
+      c.m_weight = 0;
+      char b64[28];
+      lbf_b64_27(&dig[20 * i], b64);
+      c.m_hash.assign(b64, 27);
+    }
+  }
+  ff.m_files[name] = file;
+}
+
+// The leecher's file equals the synthetic stream (a missing file equals an
+// empty stream: the leecher creates its file on the first chunk it accepts).
+bool file_matches_synthetic(const std::string& path, U64 size, unsigned threads) {
+  struct stat st;
+  if (stat(path.c_str(), &st) != 0) return size == 0;
+  if ((U64)st.st_size != size) return false;
+  const int fd = open(path.c_str(), O_RDONLY);
+  if (fd < 0) return false;
+  const U64 block = 64ull << 20;
+  std::atomic<bool> eq{true};
+  parallel_for((size + block - 1) / block, threads, [&](size_t b) {
+    const U64 off = b * block, len = std::min(block, size - off);
+    V_U8 got(len), want(len);
+    if (pread(fd, got.data(), len, (off_t)off) != (ssize_t)len) eq = false;
+    synth_bytes(want.data(), off, len);
+    if (memcmp(got.data(), want.data(), len) != 0) eq = false;
+  });
+  close(fd);
+  return eq;
+}
+
 // The leecher creates a file on its first received chunk (ChunkMethods.cpp:169-172),
 // so a zero-chunk (empty) file is never created: an empty seed file and a missing
 // leech file count as equal, as they would for the reference's peers.
@@ -289,8 +371,32 @@ void seeder_main(int lfd, FloodFileSPtr ff, std::string root, const Opts& o, See
     V_U64 offs;
     std::string valid;
     auto t0 = Clock::now();
-    if (fl.ReadVerifiedChunks(keys, arena, offs, valid) != Error::NO_ERROR_LBF)
+    if (o.synthetic) {
+      // the requested chunks from the generator, 16-byte aligned in the arena,
+      // then the same GPU re-verify before sending (ChunkMethods.cpp:116-123)
+      std::vector<Flood::ChunkArrival> chunks(keys.size());
+      offs.assign(keys.size(), 0);
+      U64 total = 0;
+      for (size_t k = 0; k < keys.size(); ++k) {
+        auto it = fl.m_runtimefiles.find(keys[k].first);
+        U32 sz = 0;
+        if (it != fl.m_runtimefiles.end() && keys[k].second < it->second.m_file->m_chunks.size())
+          sz = it->second.m_file->m_chunks[keys[k].second].m_size;
+        offs[k] = total;
+        chunks[k] = Flood::ChunkArrival{keys[k].first, keys[k].second, total, sz};
+        total += (sz + 15) & ~15ull;
+      }
+      arena.assign(total ? total : 1, 0);
+      parallel_for(keys.size(), o.threads, [&](size_t k) {
+        auto it = fl.m_runtimefiles.find(keys[k].first);
+        if (chunks[k].m_size == 0 || it == fl.m_runtimefiles.end()) return;
+        synth_bytes(&arena[offs[k]], it->second.m_chunkoffsets[keys[k].second], chunks[k].m_size);
+      });
+      if (fl.VerifyChunks(arena.data(), arena.size(), chunks, valid) != Error::NO_ERROR_LBF)
+        die("seeder: verify failed: " + std::string(Encoder::LastError()));
+    } else if (fl.ReadVerifiedChunks(keys, arena, offs, valid) != Error::NO_ERROR_LBF) {
       die("seeder: verify failed: " + std::string(Encoder::LastError()));
+    }
     auto t1 = Clock::now();
     // sizes and the (first-send-only) corruption decision, serially
     std::vector<U32> sizes(keys.size(), 0);
@@ -359,10 +465,11 @@ int main(int argc, char** argv) {
     else if (a == "--corrupt") o.corrupt = (U32)strtoul(val(), nullptr, 10);
     else if (a == "--dir") o.dir = val();
     else if (a == "--keep") o.keep = true;
+    else if (a == "--synthetic") o.synthetic = true;
     else {
       fprintf(stderr,
               "usage: lbf_loopback [--size BYTES] [--chunksize N] [--window W] [--batch B] [--threads T]\n"
-              "                    [--corrupt K] [--dir DIR] [--keep]\n");
+              "                    [--corrupt K] [--dir DIR] [--keep] [--synthetic]\n");
       return 2;
     }
   }
@@ -379,18 +486,25 @@ int main(int argc, char** argv) {
   mkdir(seeddir.c_str(), 0755);
   mkdir(leechdir.c_str(), 0755);
   struct statvfs vfs;
-  if (statvfs(o.dir.c_str(), &vfs) == 0 && (U64)vfs.f_bavail * vfs.f_frsize < 2 * o.size + (64 << 20))
-    die("not enough free space in " + o.dir + " for two copies of the file");
+  const U64 copies = o.synthetic ? 1 : 2;
+  if (statvfs(o.dir.c_str(), &vfs) == 0 && (U64)vfs.f_bavail * vfs.f_frsize < copies * o.size + (64 << 20))
+    die("not enough free space in " + o.dir + " for " + std::to_string(copies) + " copies of the file");
 
   // The seeder's file and the flood file both peers load (test_encoder + test_client).
   const std::string name = "c5.bin";
-  write_source(seeddir + "/" + name, o.size, o.threads);
-  Encoder::ToEncode te;
-  te.m_files.push_back(seeddir + "/" + name);
-  te.m_chunksize = o.chunksize;
   FloodFile encoded;
   auto te0 = Clock::now();
-  if (Encoder::EncodeFile(te, encoded) != Error::NO_ERROR_LBF) die("EncodeFile failed: " + std::string(Encoder::LastError()));
+  if (o.synthetic) {
+    encode_synthetic(seeddir + "/" + name, o.size, o.chunksize, encoded);
+  } else {
+    write_source(seeddir + "/" + name, o.size, o.threads);
+    te0 = Clock::now();
+    Encoder::ToEncode te;
+    te.m_files.push_back(seeddir + "/" + name);
+    te.m_chunksize = o.chunksize;
+    if (Encoder::EncodeFile(te, encoded) != Error::NO_ERROR_LBF)
+      die("EncodeFile failed: " + std::string(Encoder::LastError()));
+  }
   const double encode_s = secs(te0, Clock::now());
   // peers address the file by its name relative to their own directory
   FloodFileSPtr ff(new FloodFile());
@@ -585,7 +699,8 @@ int main(int argc, char** argv) {
   Flood check;
   check.m_rootdir = leechdir;
   const bool resumed = check.Initialize(leech_ff) == Error::NO_ERROR_LBF && check.m_chunkstodownload.empty();
-  const bool same = files_equal(seeddir + "/" + name, leechdir + "/" + name);
+  const bool same = o.synthetic ? file_matches_synthetic(leechdir + "/" + name, o.size, o.threads)
+                                : files_equal(seeddir + "/" + name, leechdir + "/" + name);
   std::sort(lat_us.begin(), lat_us.end());
   auto pct = [&](double p) { return lat_us.empty() ? 0.0 : lat_us[std::min(lat_us.size() - 1, (size_t)(p * lat_us.size()))]; };
   const double wall = secs(t_start, t_end);
@@ -595,13 +710,15 @@ int main(int argc, char** argv) {
          "\"leecher\": {\"batches\": %zu, \"mean_batch\": %.1f, \"decode_s\": %.3f, \"verify_write_s\": %.3f, "
          "\"rejected\": %zu, \"undecodable\": %zu}, \"seeder\": {\"requests\": %llu, \"sent\": %llu, \"refused\": %llu, \"verify_s\": %.3f, "
          "\"encode_s\": %.3f}, \"verify_latency_us\": {\"p50\": %.0f, \"p90\": %.0f, \"p99\": %.0f, \"max\": %.0f}, "
-         "\"resume_verify_complete\": %s, \"files_identical\": %s, \"corrupt_every\": %u, \"corrupted_sent\": %llu}\n",
+         "\"resume_verify_complete\": %s, \"files_identical\": %s, \"corrupt_every\": %u, \"corrupted_sent\": %llu, "
+         "\"seed_source\": \"%s\"}\n",
          (unsigned long long)o.size, o.chunksize, total, o.window, o.batch, o.threads, wall,
          payload / wall / (1u << 30), wire_bytes / wall / (1u << 30), encode_s, batches,
          batches ? (double)(accepted + rejected) / batches : 0.0, decode_s, verify_s, rejected, undecodable,
          (unsigned long long)sst.requests, (unsigned long long)sst.sent, (unsigned long long)sst.refused, sst.verify_s,
          sst.encode_s, pct(0.5), pct(0.9), pct(0.99), lat_us.empty() ? 0.0 : lat_us.back(), resumed ? "true" : "false",
-         same ? "true" : "false", o.corrupt, (unsigned long long)sst.corrupted);
+         same ? "true" : "false", o.corrupt, (unsigned long long)sst.corrupted,
+         o.synthetic ? "synthetic stream (generated on request, no seeder file)" : "file");
   if (!o.keep) {
     unlink((seeddir + "/" + name).c_str());
     unlink((leechdir + "/" + name).c_str());

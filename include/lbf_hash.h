@@ -61,12 +61,23 @@ const char* lbf_last_error(void);
 int lbf_device_count(int* out_count);
 /* device_mask bit d selects device d; 0 selects every visible device.
  * Fails with LBF_ERR_NO_DEVICE when no GPU is visible.  Host-path staging,
- * read at creation: LBF_SLOTS slots per device (2..8, default 3), each grown
+ * read at creation: LBF_SLOTS slots per worker (2..8, default 3), each grown
  * on demand up to LBF_SLOT_MB MiB (default 512); LBF_COPY_THREADS host copy
- * threads (default 8). */
+ * threads (default 8).  Pinned staging is allocated on the GPU's NUMA node and
+ * the copy threads run on that node's CPUs (LBF_NUMA=0 turns this off). */
 int lbf_ctx_create(uint32_t device_mask, lbf_ctx** out_ctx);
 void lbf_ctx_destroy(lbf_ctx* ctx);
 int lbf_ctx_num_devices(const lbf_ctx* ctx);
+/* Host-path workers: one per selected device (LBF_WORKERS_PER_DEVICE=k, a
+ * test knob read at creation, gives k per device).  A batch is split into
+ * contiguous index ranges, one per worker, each on its own host thread. */
+int lbf_ctx_num_workers(const lbf_ctx* ctx);
+/* Placement of worker `worker` (diagnostics): its device, that device's NUMA
+ * node (-1 unknown or LBF_NUMA=0), the NUMA node holding its pinned staging
+ * (-1 unknown), and how many CPUs its host threads are bound to (0 unbound).
+ * Any output pointer may be NULL. */
+int lbf_ctx_worker_info(const lbf_ctx* ctx, int worker, int* device, int* numa_node, int* staging_node,
+                        int* bound_cpus);
 
 /* ---- batched chunk hashing (Encoder::EncodeFile's per-chunk hash) --------
  * Chunk i is the byte range [offsets[i], offsets[i] + sizes[i]) of `base`.

@@ -12,7 +12,9 @@ oracle/sha1_oracle.c (oracle_synth_word) and in the device fill kernel; small
 streams are generated here with numpy, the 4 GiB C2 stream with the oracle's
 C filler (cross-checked against numpy on a prefix before use).
 
-Run:  python tests/golden/make_golden.py        (takes ~1 minute)
+Run:  python tests/golden/make_golden.py          (takes ~1 minute)
+      python tests/golden/make_golden.py --ranks  (c2_ranks.json: the 8 weak-scaled C2 shards, ~5 minutes)
+      python tests/golden/make_golden.py --big    (c3.json, c4.json: 64 GiB + 256 GiB, ~1 hour)
 """
 import base64
 import ctypes
@@ -141,6 +143,26 @@ def big(lib):
     })
 
 
+def ranks(lib, world=8):
+    """The weak-scaled C2 stream bench.py hashes at N GPUs: rank r hashes bytes
+    [r*4 GiB, (r+1)*4 GiB) of stream 0x5EED at 256 KiB chunks, for r < world.
+    Rank 0 is C2 itself (cross-checked against c2.json)."""
+    size, cs = 4 << 30, 262144
+    out = []
+    for r in range(world):
+        d = stream_digests(lib, SEED_C, r * size, size, cs)
+        out.append({"rank": r, "first_chunk": r * (size // cs), "n_chunks": len(d),
+                    "sha1_of_concat_raw_digests_hex": dod(d),
+                    "samples_b64": {str(i): b64_27(d[i]) for i in (0, 1, 8191, len(d) - 1)}})
+        print(f"  C2 rank {r}", end="\r", file=sys.stderr)
+    with open(os.path.join(HERE, "c2.json")) as f:
+        assert json.load(f)["sha1_of_concat_raw_digests_hex"] == out[0]["sha1_of_concat_raw_digests_hex"]
+    write("c2_ranks.json", {
+        "config": "bench.py weak scaling: rank r hashes bytes [r*4GiB,(r+1)*4GiB) of stream 0x5EED, 256 KiB chunks",
+        "seed": SEED_C, "bytes_per_rank": size, "chunk_size": cs, "ranks": out,
+    })
+
+
 def write(name, obj):
     with open(os.path.join(HERE, name), "w") as f:
         json.dump(obj, f, indent=1, sort_keys=True)
@@ -257,5 +279,7 @@ def main():
 if __name__ == "__main__":
     if "--big" in sys.argv:
         big(load_oracle())
+    elif "--ranks" in sys.argv:
+        ranks(load_oracle())
     else:
         main()

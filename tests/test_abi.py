@@ -64,6 +64,22 @@ def test_no_gpu_fails_loudly():
     assert "no CPU fallback" in str(ei.value)
 
 
+def test_shipped_kernel_variants_only():
+    """The product library carries the four shipped kernels (1 lane, 7 pc4/b64,
+    10 pcx5, 11 lds2); the superseded ones exist only in the experimental build."""
+    lib = _capi.load()
+    try:
+        for v in (0, 1, 7, 10, 11):
+            assert lib.lbf_set_kernel_variant(v) == _capi.LBF_OK, v
+        for v in (2, 3, 4, 5, 6, 8, 9, 12, -1):
+            assert lib.lbf_set_kernel_variant(v) == _capi.LBF_ERR_INVALID, v
+        # automatic choice by chain count (DESIGN.md §4.4)
+        lib.lbf_set_kernel_variant(0)
+        assert [lib.lbf_kernel_for(n) for n in (1, 16384, 16385, 32768, 32769, 1 << 20)] == [7, 7, 10, 10, 11, 11]
+    finally:
+        lib.lbf_set_kernel_variant(0)
+
+
 def test_kernels_compiled_for_gfx950():
     blob = open(_capi.LIB_PATH, "rb").read()
     assert b"amdgcn-amd-amdhsa--gfx950" in blob

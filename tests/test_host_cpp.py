@@ -92,22 +92,14 @@ def test_loopback_needs_gpu():
     assert out.returncode == 2 and "no CPU fallback" in out.stderr
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("size,cs,window,batch,corrupt", [
-    (64 << 20, 262144, 64, 16, 0),                 # C5 chunk size, small file
-    ((16 << 20) + 12345, 65536, 512, 128, 7),      # odd tail, wire corruption every 7th chunk
-    (3 * 262144 + 1, 262144, 1, 1, 0),             # one chunk in flight, batch of one
-    (65537, 4096, 1, 3, 1),                        # every chunk corrupted on its first send
-    (0, 1000, 1024, 512, 0),                       # empty file: no chunks, nothing to create
-])
-def test_loopback_two_peers(tmp_path, size, cs, window, batch, corrupt):
-    """C5 shape: seeder and leecher over 127.0.0.1 speaking the reference's frames;
-    every arrival is GPU-verified before it is written; a corrupted arrival is
-    rejected and fetched again; the written file passes the resume verify and
-    equals the source byte for byte."""
-    out = subprocess.run([os.path.join(LIB, "lbf_loopback"), "--size", str(size), "--chunksize", str(cs),
-                          "--window", str(window), "--batch", str(batch), "--corrupt", str(corrupt),
-                          "--dir", str(tmp_path / "c5")], capture_output=True, text=True, timeout=600)
+def _loopback(tmp_path, size, cs, window, batch, corrupt, synthetic=False, threads=None, timeout=600):
+    args = [os.path.join(LIB, "lbf_loopback"), "--size", str(size), "--chunksize", str(cs), "--window", str(window),
+            "--batch", str(batch), "--corrupt", str(corrupt), "--dir", str(tmp_path / "c5")]
+    if synthetic:
+        args.append("--synthetic")
+    if threads:
+        args += ["--threads", str(threads)]
+    out = subprocess.run(args, capture_output=True, text=True, timeout=timeout)
     assert out.returncode == 0, out.stderr + out.stdout
     r = json.loads(out.stdout.strip().splitlines()[-1])
     assert r["resume_verify_complete"] and r["files_identical"]
@@ -118,6 +110,45 @@ def test_loopback_two_peers(tmp_path, size, cs, window, batch, corrupt):
         assert r["leecher"]["rejected"] == r["corrupted_sent"]
     else:
         assert r["leecher"]["rejected"] == 0
+    return r
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("size,cs,window,batch,corrupt,synthetic", [
+    (64 << 20, 262144, 64, 16, 0, False),                 # C5 chunk size, small file
+    ((16 << 20) + 12345, 65536, 512, 128, 7, False),      # odd tail, wire corruption every 7th chunk
+    ((16 << 20) + 12345, 65536 + 3, 512, 128, 7, True),   # generated seeder, chunks off the 8-byte grid
+    (3 * 262144 + 1, 262144, 1, 1, 0, False),             # one chunk in flight, batch of one
+    (65537, 4096, 1, 3, 1, False),                        # every chunk corrupted on its first send
+    (65537, 4096, 1, 3, 1, True),
+    (0, 1000, 1024, 512, 0, False),                       # empty file: no chunks, nothing to create
+    (0, 1000, 1024, 512, 0, True),
+])
+def test_loopback_two_peers(tmp_path, size, cs, window, batch, corrupt, synthetic):
+    """C5 shape: seeder and leecher over 127.0.0.1 speaking the reference's frames;
+    every arrival is GPU-verified before it is written; a corrupted arrival is
+    rejected and fetched again; the written file passes the resume verify and
+    equals the source (a file, or with --synthetic the generated stream) byte
+    for byte."""
+    _loopback(tmp_path, size, cs, window, batch, corrupt, synthetic)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+def test_c5_full_size_16gib(tmp_path):
+    """C5 at its stated workload (BASELINE.json configs[4]): 16 GiB at the
+    test_encoder default of 256 KiB chunks, i.e. 65,536 chunks, each verified on
+    the GPU on receipt (ChunkMethods.cpp:137-225) before it is written, with
+    every 1000th chunk corrupted on the wire once.  The seeder serves the
+    generated stream (no 16 GiB seeder file); the leecher's 16 GiB file must pass
+    the resume verify and equal the stream.  Not in the harness, on purpose: the
+    tracker hop (test_tracker.cpp:27-75, TrackerMethods.cpp:26-44), the
+    NotifyHaveChunk broadcast (ChunkMethods.cpp:202-211) and the 100 ms loop
+    pacing (test_client.cpp:72-76) -- control plane, not the hash path."""
+    r = _loopback(tmp_path, 16 << 30, 262144, 4096, 1024, 1000, synthetic=True, threads=16, timeout=840)
+    assert r["chunks"] == 65536 and r["corrupted_sent"] == 65
+    print("C5 16 GiB:", json.dumps({k: r[k] for k in ("seconds", "payload_gibs", "wire_gibs", "verify_latency_us",
+                                                        "leecher", "seeder", "encode_flood_s")}))
 
 
 def test_expected_xml_helper_matches_cpp_unit_case():

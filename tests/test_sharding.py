@@ -70,3 +70,67 @@ def test_gloo_two_ranks_gather_equals_single(tmp_path, oracle, world):
         got = np.load(tmp_path / f"r{r}.npy")
         assert np.array_equal(got, want)
         assert float((tmp_path / f"t{r}.txt").read_text()) == float(world)
+
+
+# --------------------------------------------------------------------------- bench self-validation
+def test_c2_rank_goldens_agree_with_oracle(oracle, golden):
+    """tests/golden/c2_ranks.json (hashlib) pins rank r's shard of the
+    weak-scaled C2 stream; its sampled chunks must equal the oracle's hash of
+    the same stream bytes, and rank 0 must be C2 itself."""
+    from tests.golden.make_golden import b64_27 as ref_b64
+    g = golden("c2_ranks.json")
+    cs, per = g["chunk_size"], g["bytes_per_rank"]
+    assert [r["rank"] for r in g["ranks"]] == list(range(8))
+    assert g["ranks"][0]["sha1_of_concat_raw_digests_hex"] == golden("c2.json")["sha1_of_concat_raw_digests_hex"]
+    for r in g["ranks"]:
+        assert r["first_chunk"] == r["rank"] * (per // cs) and r["n_chunks"] == per // cs
+        for k, want in r["samples_b64"].items():
+            chunk = oracle.synth(g["seed"], r["rank"] * per + int(k) * cs, cs)
+            assert ref_b64(oracle.sha1(chunk)) == want, (r["rank"], k)
+
+
+def _bench_parity_worker(rank, world, port, out_dir, corrupt_rank):
+    import json as _json
+
+    import torch.distributed as dist
+
+    import bench
+    from tests.oracle_lib import Oracle
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    orc = Oracle()
+    gold = _json.load(open(os.path.join(out_dir, "gold.json")))["ranks"][rank]
+    cs = 4096
+    data = orc.synth(0x5EED, rank * 64 * cs, 64 * cs)
+    d = orc.encode_buffer(data, cs)
+    if rank == corrupt_rank:
+        d[5, 0] ^= 1
+    flags = bench.gather_ints(bench.check_golden(gold, d), world)
+    with open(os.path.join(out_dir, f"flags{rank}.json"), "w") as f:
+        _json.dump(flags, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("corrupt_rank", [-1, 1])
+def test_bench_per_rank_parity_gather_gloo(tmp_path, oracle, corrupt_rank):
+    """bench.py's self-validation on world_size 2 (gloo): every rank checks its
+    shard against its golden entry and the flags are all-gathered; one rank with
+    a wrong digest shows up as 0 in every rank's list."""
+    import json as _json
+
+    from tests.golden.make_golden import b64_27 as ref_b64
+    import hashlib
+    cs = 4096
+    ranks = []
+    for r in range(2):
+        d = oracle.encode_buffer(oracle.synth(0x5EED, r * 64 * cs, 64 * cs), cs)
+        ranks.append({"rank": r, "n_chunks": 64, "sha1_of_concat_raw_digests_hex": hashlib.sha1(d.tobytes()).hexdigest(),
+                      "samples_b64": {"0": ref_b64(bytes(d[0])), "63": ref_b64(bytes(d[63]))}})
+    (tmp_path / "gold.json").write_text(_json.dumps({"ranks": ranks}))
+    mp.spawn(_bench_parity_worker, args=(2, _free_port(), str(tmp_path), corrupt_rank), nprocs=2, join=True)
+    want = [1, 1] if corrupt_rank < 0 else [1, 0]
+    for r in range(2):
+        assert _json.loads((tmp_path / f"flags{r}.json").read_text()) == want

@@ -5,6 +5,8 @@
 //     ../bitflood_amd/host/{PeerWire,FloodFile,Encoder,Flood}.cpp -L../bitflood_amd/lib -llbfhash -o build/fuzz_wire
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
+#include <memory>
 #include <random>
 #include <string>
 #include <vector>
@@ -50,9 +52,13 @@ int main(int argc, char** argv) {
     U32 idx = 0;
     size_t n = 0;
     std::vector<U8> out(4096);
-    if (PeerWire::DecodeSendChunk(s.data(), s.size(), fname, idx, out.data(), out.size(), n)) checks += n <= out.size();
+    // (ptr, len) APIs get an exact-size heap copy with no terminator, so ASAN
+    // sees any read past `len` (a std::string's data() is NUL-terminated).
+    std::unique_ptr<char[]> raw(new char[s.size()]);
+    if (!s.empty()) memcpy(raw.get(), s.data(), s.size());
+    if (PeerWire::DecodeSendChunk(raw.get(), s.size(), fname, idx, out.data(), out.size(), n)) checks += n <= out.size();
     std::vector<U8> small(7);
-    PeerWire::Base64Get(s.data(), s.size(), small.data(), small.size());
+    PeerWire::Base64Get(raw.get(), s.size(), small.data(), small.size());
     FloodFile f;
     f.FromXML(s);
     ++checks;

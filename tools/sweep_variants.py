@@ -6,6 +6,9 @@ several chunk counts and chunk sizes over one device-resident synthetic region,
 including the C3 shape (64 GiB at 256 KiB = 262,144 chunks) and the per-GPU C4
 shape (32 GiB at 1 MiB = 32,768 chunks).  Prints one JSON line per point.
 Usage: python tools/sweep_variants.py [--max-gib 64] [--reps 3]
+Superseded variants (2-6, 8, 9) need the experimental build:
+  make -C bitflood_amd/csrc experimental
+  LBF_LIB=bitflood_amd/lib/experimental/liblbfhash.so python tools/sweep_variants.py --variants 4,7
 """
 import argparse
 import hashlib
@@ -30,7 +33,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--max-gib", type=int, default=64)
     ap.add_argument("--reps", type=int, default=3)
-    ap.add_argument("--variants", default="1,2,3")
+    ap.add_argument("--variants", default="1,7,10,11")
     a = ap.parse_args()
     size = a.max_gib * GIB
     buf = DeviceBuffer(size)
