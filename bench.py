@@ -210,6 +210,18 @@ def cpu_baseline(args, stream_start, n_chunks_sample, gpu_digests_sample):
     }, data
 
 
+def _host_desc():
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except Exception:
+        pass
+    return {"cpu_model": model, "os_cpu_count": os.cpu_count()}
+
+
 def compute_floor_ms(variant, cs, n_chunks):
     """Lower bound on one launch from instruction issue alone (SHA-1 is a serial
     chain per chunk, so few chunks are bound by one chain's issue rate)."""

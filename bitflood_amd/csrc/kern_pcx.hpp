@@ -334,6 +334,9 @@ __global__ void __launch_bounds__(256) sha1_pcx5_kernel(ChunkParams p) {
   const uint32_t nsteps = __builtin_amdgcn_readfirstlane(wg_steps);
   if (nsteps == 0) return;  // uniform over the workgroup
 
+#ifdef LBF_PC_STAMPS
+  unsigned long long acc[4] = {0, 0, 0, 0}, t0 = 0, t1 = 0, t2 = 0;
+#endif
   if (wave >= 2) {
     // ---------------- producer ----------------
     const uint32_t raw_lds = (uint32_t)reinterpret_cast<uintptr_t>(raw_base);
@@ -344,8 +347,13 @@ __global__ void __launch_bounds__(256) sha1_pcx5_kernel(ChunkParams p) {
     __syncthreads();  // barrier P: steps 0 and 1 complete
     __syncthreads();  // barrier 0: the consumers hold step 0
     for (uint32_t k = 0; k + 1 < nsteps; ++k) {
+      PC_STAMP(t0);
       if (k + 2 < nsteps) px5_produce<kKFrom>(ring, raw_lds, c, k + 2, lane);
+      PC_STAMP(t1);
       __syncthreads();  // barrier k+1
+      PC_STAMP(t2);
+      PC_ACC(1, t0, t1);  // producer: work (incl. its vmcnt wait)
+      PC_ACC(2, t1, t2);  // producer: barrier
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA outlives the workgroup
   } else {
@@ -355,7 +363,6 @@ __global__ void __launch_bounds__(256) sha1_pcx5_kernel(ChunkParams p) {
     const RoundK K;
     Px5Sched A, B;
 #ifdef LBF_PC_STAMPS
-    unsigned long long acc[4] = {0, 0, 0, 0};
 #define PX5_ACC , acc
 #else
 #define PX5_ACC
@@ -391,6 +398,15 @@ __global__ void __launch_bounds__(256) sha1_pcx5_kernel(ChunkParams p) {
     if (i < p.n) write_result(p, i, s);
 #undef PX5_ACC
   }
+#ifdef LBF_PC_STAMPS
+  if (lane == 0) {  // [wg][wave][0..3]: consumer {barrier wait, -, -, steps}; producer {-, work, barrier, steps}
+    unsigned long long* o = g_pc_stamps + (blockIdx.x * 4 + wave) * 4;
+    o[0] = acc[0];
+    o[1] = acc[1];
+    o[2] = acc[2];
+    o[3] = nsteps;
+  }
+#endif
 }
 
 // K split for pcx5: the consumer adds K in rounds 0..63.  With the producer's

@@ -5,6 +5,7 @@
 # stopping at the first step that fails.  Logs land in gpurun_out/<tag>/.
 set -o pipefail
 tag=${1:-run}
+only=${2:-}  # optional pytest -k expression
 out=gpurun_out/$tag
 mkdir -p "$out"
 export TMPDIR=${TMPDIR:-/tmp}
@@ -17,7 +18,7 @@ step() {  # step <name> <seconds> <cmd...>
   tail -n 5 "$out/$name.log"
   return $rc
 }
-step pytest_gpu 700 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -p no:cacheprovider &&
+step pytest_gpu 700 python -u -m pytest tests -m gpu -v -rP --durations=15 --timeout 300 --timeout-method thread -p no:cacheprovider ${only:+-k "$only"} &&
 step latency 120 bitflood_amd/lib/lbf_latency --reps 200 &&
 step bench_c2 300 python bench.py --steps 20 --warmup 5 &&
 step bench_2rank_gloo 300 env LBF_BENCH_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \

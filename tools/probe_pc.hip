@@ -18,38 +18,48 @@ static void run(int variant, uint8_t* buf, uint64_t len, uint32_t cs, uint8_t* d
     printf("error: %s\n", lbf_last_error());
     return;
   }
-  const int wgs = (int)((n + 63) / 64);
-  const int nw = (variant == 4 || variant == 6) ? 3 : 2;  // waves per workgroup
+  const bool px = variant == 10;  // two pairs per workgroup: waves 0,1 consume, 2,3 produce
+  const int wgs = (int)((n + (px ? 127 : 63)) / (px ? 128 : 64));
+  const int nw = (variant == 4 || variant == 6 || variant == 7) ? 3 : px ? 4 : 2;  // waves per workgroup
   std::vector<unsigned long long> h(wgs * nw * 4);
   hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(lbf::g_pc_stamps), wgs * nw * 4 * 8, 0, hipMemcpyDeviceToHost);
   double a[3][3] = {{0}};
   double steps = 0;
+  // roles: 0 = consumer(s), 1.. = producer(s); pcx5's two pairs fold into one consumer and one producer
+  const int roles = px ? 2 : nw;
   for (int w = 0; w < wgs; ++w)
     for (int r = 0; r < nw; ++r) {
-      for (int j = 0; j < 3; ++j) a[r][j] += (double)h[(w * nw + r) * 4 + j];
+      const int role = px ? (r >= 2 ? 1 : 0) : r;
+      for (int j = 0; j < 3; ++j) a[role][j] += (double)h[(w * nw + r) * 4 + j] / (px ? 2 : 1);
       if (r == 0) steps += (double)h[(w * nw) * 4 + 3];
     }
   steps /= wgs;
-  for (int r = 0; r < nw; ++r)
+  for (int r = 0; r < roles; ++r)
     for (int j = 0; j < 3; ++j) a[r][j] /= wgs * steps;
   printf("variant %d cs=%u n=%lu: %.3f ms (%.1f GiB/s)  steps=%.0f  cycles/step: consumer[wait %.0f work %.0f]",
          variant, cs, (unsigned long)n, ms, len / (ms * 1e-3) / (1 << 30), steps, a[0][0], a[0][1]);
-  for (int r = 1; r < nw; ++r)
+  for (int r = 1; r < roles; ++r)
     printf(" producer%d[vmwait %.0f work %.0f barrier %.0f]", r - 1, a[r][0], a[r][1], a[r][2]);
   printf("\n");
 }
 
-int main() {
-  const uint64_t len = 4ull << 30;
+int main(int argc, char** argv) {
+  // default: pcx5 at the C4 shape (32,768 x 1 MiB, 32 GiB) and at 32,768 x 256 KiB, pc4 at C2
+  const uint64_t len = 32ull << 30;
   uint8_t *buf, *dig;
-  hipMalloc(&buf, len);
-  hipMalloc(&dig, (len / 65536) * 20);
+  if (hipMalloc(&buf, len) != hipSuccess || hipMalloc(&dig, (len / 65536) * 20) != hipSuccess) {
+    printf("hipMalloc failed\n");
+    return 1;
+  }
   lbf_fill_synthetic(buf, len, 0x5EED, 0, nullptr);
   hipDeviceSynchronize();
-  for (int v : {4, 6}) {
-    run(v, buf, len, 262144, dig);
-    run(v, buf, len / 2, 262144, dig);
-    run(v, buf, len, 1 << 20, dig);
-  }
+  const bool all = argc > 1;
+  run(10, buf, len, 1 << 20, dig);
+  run(10, buf, 8ull << 30, 262144, dig);
+  run(7, buf, 4ull << 30, 262144, dig);
+  if (all)
+    for (int v : {4, 6}) run(v, buf, 4ull << 30, 262144, dig);
+  hipFree(buf);
+  hipFree(dig);
   return 0;
 }
