@@ -197,6 +197,21 @@ def cpu_baseline(args, stream_start, n_chunks_sample, gpu_digests_sample):
     d_1 = orc.sha1_batch(data, offs[:n1], sizes[:n1], nthreads=1)
     t_1 = time.perf_counter() - t0
     st_gibs = n1 * cs / GIB / t_1
+    # fread-inclusive single-thread encode of the same bytes as a file, as
+    # Encoder::EncodeFile does it (one chunk buffer, fread + hash per chunk;
+    # oracle_encode_file); the file is page-cache warm, written just before
+    import tempfile
+    fread = None
+    with tempfile.NamedTemporaryFile(prefix="lbf_cpu_sample_", dir=os.environ.get("TMPDIR", "/tmp")) as f:
+        data[: n1 * cs].tofile(f.name)
+        dig = np.zeros((n1, 20), dtype=np.uint8)
+        t0 = time.perf_counter()
+        got = orc.lib.oracle_encode_file(f.name.encode(), cs, dig.ctypes.data, n1, None)
+        t_f = time.perf_counter() - t0
+        if got == n1:
+            fread = {"value": round(n1 * cs / GIB / t_f, 3), "unit": "GiB/s",
+                     "sample": f"{n1} x {cs // 1024} KiB chunks from a page-cached file, 1 thread",
+                     "parity_vs_gpu": bool(np.array_equal(dig, gpu_digests_sample[:n1]))}
     parity = bool(np.array_equal(d_mt, gpu_digests_sample) and np.array_equal(d_1, gpu_digests_sample[:n1]))
     return {
         "value": round(mt_gibs, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
@@ -204,6 +219,7 @@ def cpu_baseline(args, stream_start, n_chunks_sample, gpu_digests_sample):
                   f"{reps} pass(es) on {threads} threads; single-thread pass over {n1} chunks",
         "single_thread_value": round(st_gibs, 3),
         "affinity_threads_value": round(aff_gibs, 3),
+        "single_thread_fread_encode": fread,
         "host": {**_host_desc(), "affinity_cores": affinity, "cgroup_cpu_quota": quota, "usable_cores": usable,
                  "numa_nodes": _numa_nodes()},
         "parity_vs_gpu": parity,

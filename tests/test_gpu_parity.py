@@ -308,3 +308,22 @@ def test_chunk_over_512_mib_bit_length_high_word(oracle):
         buf.free()
         dig.free()
     assert got == hashlib.sha1(oracle.synth(91, 0, n_bytes, nthreads=8).tobytes()).digest()
+
+
+def test_more_chunks_than_one_group_holds(hasher, oracle):
+    """150,000 small chunks in one call: more than a staging group's 65,536
+    descriptors, so the job spans several groups by count, not by bytes; sizes
+    0..600 cover every padding case, offsets are unaligned; hash and verify."""
+    rng = np.random.default_rng(150000)
+    n = 150000
+    sizes = rng.integers(0, 601, n).astype(np.uint32)
+    buf = oracle.synth(67, 0, int(sizes.sum()) + 4096, nthreads=8)
+    offs = np.concatenate([[0], np.cumsum(sizes[:-1], dtype=np.uint64)]).astype(np.uint64) + np.uint64(3)
+    want = oracle.sha1_batch(buf, offs, sizes, nthreads=8)
+    got = hasher.hash_chunks(buf, offs, sizes)
+    bad = np.flatnonzero((got != want).any(axis=1))
+    assert bad.size == 0, bad[:10]
+    exp = want.copy()
+    flips = [0, 65535, 65536, 131072, n - 1]
+    exp[flips, 11] ^= 0x80
+    assert np.flatnonzero(~hasher.verify_chunks(buf, offs, sizes, exp)).tolist() == flips

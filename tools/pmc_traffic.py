@@ -40,6 +40,7 @@ def main():
     ap.add_argument("src")
     ap.add_argument("dst")
     ap.add_argument("--file-bytes", type=int, default=4 << 30)
+    ap.add_argument("--chunk-size", type=int, default=262144)
     ap.add_argument("--kernel", default="sha1_")
     ap.add_argument("--record", action="store_true")
     a = ap.parse_args()
@@ -94,12 +95,23 @@ def main():
         json.dump(out, f, indent=1)
     print(json.dumps(out, indent=1))
     if a.record and "hbm_bytes_per_launch" in out:
+        # one entry per (file size, chunk size, kernel): bench.py looks its workload up here
         root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-        rec = {"file_bytes": a.file_bytes, "hbm_bytes_per_launch": out["hbm_bytes_per_launch"],
+        path = os.path.join(root, "profiles", "pmc_traffic.json")
+        rec = {"file_bytes": a.file_bytes, "chunk_size": a.chunk_size,
+               "hbm_bytes_per_launch": out["hbm_bytes_per_launch"],
                "source": os.path.relpath(os.path.join(a.dst, "summary.json"), root),
                "kernel": out.get("kernel")}
-        with open(os.path.join(root, "profiles", "pmc_traffic.json"), "w") as f:
-            json.dump(rec, f, indent=1)
+        try:
+            old = json.load(open(path))
+            entries = old.get("entries", [old])
+        except (OSError, ValueError):
+            entries = []
+        entries = [e for e in entries if not (e.get("file_bytes") == a.file_bytes
+                                              and e.get("chunk_size", 262144) == a.chunk_size
+                                              and e.get("kernel") == rec["kernel"])]
+        with open(path, "w") as f:
+            json.dump({"entries": entries + [rec]}, f, indent=1)
 
 
 if __name__ == "__main__":
