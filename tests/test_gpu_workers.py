@@ -10,6 +10,7 @@ box, so that branch runs here exactly as it would with one worker per device.
 Results are compared with the oracle, bit for bit.
 """
 import hashlib
+import json
 import os
 import subprocess
 
@@ -145,6 +146,17 @@ def test_numa_placement(monkeypatch):
         h.close()
 
 
+def test_numa_placement_off():
+    """LBF_NUMA=0: no node, no binding (read once per process, so a child)."""
+    code = ("import torch, json; from bitflood_amd import ChunkHasher\n"
+            "h = ChunkHasher(); print(json.dumps(h.worker_info(0))); h.close()")
+    out = subprocess.run(["python", "-c", code], cwd=ROOT, capture_output=True, text=True, timeout=120,
+                         env={**os.environ, "LBF_NUMA": "0"})
+    assert out.returncode == 0, out.stderr
+    info = json.loads(out.stdout.strip().splitlines()[-1])
+    assert info["numa_node"] == -1 and info["bound_cpus"] == 0, info
+
+
 def _sysfs_gpu_node():
     """NUMA node of GPU 0 from sysfs, read independently of the library."""
     out = subprocess.run(["rocm-smi", "--showbus"], capture_output=True, text=True)
@@ -167,9 +179,10 @@ def test_encode_file_cli_multi_worker(workers, tmp_path, oracle, golden):
     c1 = golden("c1.json")
     (tmp_path / "c1.bin").write_bytes(oracle.synth(c1["seed"], 0, c1["size"]).tobytes())
     env = {**os.environ, "LBF_WORKERS_PER_DEVICE": str(workers), "LBF_SLOT_MB": "2"}
+    # --devices 1: Encoder::SetDeviceMask(1) before first use, then k workers on device 0
     out = subprocess.run([os.path.join(LIB, "lbf_encoder"), "c1.bin", "http://127.0.0.1:10101/", "c1.flood",
-                          "--chunksize", str(c1["chunk_size"])], cwd=tmp_path, capture_output=True, text=True,
-                         env=env, timeout=120)
+                          "--chunksize", str(c1["chunk_size"]), "--devices", "1"], cwd=tmp_path, capture_output=True,
+                         text=True, env=env, timeout=120)
     assert out.returncode == 0, out.stderr
     chunks = [(hh, i, c1["chunk_size"], 0) for i, hh in enumerate(c1["b64"])]
     assert (tmp_path / "c1.flood").read_text() == expected_xml([("c1.bin", c1["size"], chunks)],
@@ -178,7 +191,7 @@ def test_encode_file_cli_multi_worker(workers, tmp_path, oracle, golden):
     bad = bytearray(data)
     bad[37 * c1["chunk_size"] + 3] ^= 1
     (tmp_path / "c1.bin").write_bytes(bytes(bad))
-    out = subprocess.run([os.path.join(LIB, "lbf_verify"), "c1.flood", "--no-resolve"], cwd=tmp_path,
+    out = subprocess.run([os.path.join(LIB, "lbf_verify"), "c1.flood", "--no-resolve", "--devices", "1"], cwd=tmp_path,
                          capture_output=True, text=True, env=env, timeout=120)
     assert out.returncode == 0, out.stderr
     lines = dict(line.split(" ", 1) for line in out.stdout.strip().splitlines())
