@@ -189,9 +189,9 @@ template <int kKFrom>
 void launch_pcx4(const ChunkParams& p, hipStream_t stream) {
   static std::once_flag once;
   std::call_once(once, [] {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pcx4_kernel<false, kKFrom>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pcx4_kernel<false, kKFrom>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, kPx4LdsBytes);
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pcx4_kernel<true, kKFrom>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pcx4_kernel<true, kKFrom>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, kPx4LdsBytes);
   });
   const uint32_t blocks = (p.n + 2 * kPcLanes - 1) / (2 * kPcLanes);
@@ -420,9 +420,9 @@ template <int kKFrom>
 void launch_pcx5(const ChunkParams& p, hipStream_t stream) {
   static std::once_flag once;
   std::call_once(once, [] {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pcx5_kernel<false, kKFrom>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pcx5_kernel<false, kKFrom>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, kPx5LdsBytes);
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pcx5_kernel<true, kKFrom>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pcx5_kernel<true, kKFrom>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, kPx5LdsBytes);
   });
   const uint32_t blocks = (p.n + 2 * kPcLanes - 1) / (2 * kPcLanes);

@@ -105,7 +105,7 @@ void launch_pc4(const ChunkParams& p, hipStream_t stream, int kvec) {
                           reinterpret_cast<const void*>(&sha1_pc4_kernel<kUniform, 1>),
 #endif
                          })
-      hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kPc4LdsBytes);
+      (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kPc4LdsBytes);
   });
   const dim3 g((p.n + kPcLanes - 1) / kPcLanes), b(192);
 #ifdef LBF_EXPERIMENTAL_VARIANTS
@@ -126,7 +126,7 @@ template <bool kUniform>
 void launch_lds2(const ChunkParams& p, hipStream_t stream) {
   static std::once_flag once;
   std::call_once(once, [] {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_lds2_kernel<kUniform>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_lds2_kernel<kUniform>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, kLds2Bytes);
   });
   hipLaunchKernelGGL(sha1_lds2_kernel<kUniform>, dim3((p.n + 255) / 256), dim3(256), kLds2Bytes, stream, p);
@@ -151,9 +151,9 @@ bool launch_experimental(int variant, const ChunkParams& p, hipStream_t stream) 
     constexpr int lds = 2 * pc_lds_bytes<2>();
     static std::once_flag once;
     std::call_once(once, [] {
-      hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc_kernel<false, 2, 2>),
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc_kernel<false, 2, 2>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-      hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc_kernel<true, 2, 2>),
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc_kernel<true, 2, 2>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     });
     const uint32_t blocks = (p.n + 2 * kPcLanes - 1) / (2 * kPcLanes);
@@ -162,9 +162,9 @@ bool launch_experimental(int variant, const ChunkParams& p, hipStream_t stream) 
   } else if (variant == 4) {
     static std::once_flag once;
     std::call_once(once, [] {
-      hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc2_kernel<false>),
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc2_kernel<false>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, kP2LdsBytes);
-      hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc2_kernel<true>),
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc2_kernel<true>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, kP2LdsBytes);
     });
     const uint32_t blocks = (p.n + kPcLanes - 1) / kPcLanes;

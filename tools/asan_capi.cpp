@@ -1,0 +1,150 @@
+// tools/asan_capi.cpp -- diagnostic (not product code): randomized stress of the
+// C ABI's host paths (include/lbf_hash.h) in a build whose HOST code carries
+// AddressSanitizer + UBSan (tools/asan_build.sh; device code is not
+// instrumented).  Each case draws a context shape (workers per device,
+// staging slots, slot size, an injected one-shot group fault) and a batch
+// (ragged, unaligned, empty and oversize chunks), then checks
+//   lbf_sha1_batch / lbf_verify_batch (host memory) and
+//   lbf_file_ranges (hash and verify, including a truncated file)
+// against the oracle (oracle/sha1_oracle.c, compiled in as the checker).
+//   asan_capi <scratch-dir> [seconds] [seed]
+#include <fcntl.h>
+#include <unistd.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "lbf_hash.h"
+
+extern "C" {
+void oracle_sha1(const uint8_t* data, uint32_t len, uint8_t out[20]);
+void oracle_synth_fill_mt(uint8_t* out, uint64_t len, uint64_t seed, uint64_t start, int nthreads);
+}
+
+static int g_fail = 0;
+#define CHECK(cond, ...)                                                  \
+  do {                                                                    \
+    if (!(cond)) {                                                        \
+      std::fprintf(stderr, "CHECK failed %s:%d: %s: ", __FILE__, __LINE__, #cond); \
+      std::fprintf(stderr, __VA_ARGS__);                                  \
+      std::fprintf(stderr, "\n");                                         \
+      ++g_fail;                                                           \
+    }                                                                     \
+  } while (0)
+
+int main(int argc, char** argv) {
+  if (argc < 2) {
+    std::fprintf(stderr, "usage: asan_capi <scratch-dir> [seconds] [seed]\n");
+    return 2;
+  }
+  const std::string dir = argv[1];
+  const double budget = argc > 2 ? atof(argv[2]) : 60.0;
+  const uint64_t seed = argc > 3 ? strtoull(argv[3], nullptr, 10) : 1;
+  std::mt19937_64 rng(seed);
+  auto uni = [&](uint64_t lo, uint64_t hi) { return lo + rng() % (hi - lo + 1); };
+  const auto t_end = std::chrono::steady_clock::now() + std::chrono::duration<double>(budget);
+  long cases = 0, chunks_checked = 0, faults = 0;
+  const std::string path = dir + "/asan_capi.bin";
+
+  while (std::chrono::steady_clock::now() < t_end && g_fail == 0) {
+    // ---- context shape (environment read at creation) ----
+    const int workers = (int)uni(1, 4), slots = (int)uni(2, 5), slot_mb = (int)(uni(0, 3) == 0 ? 1 : uni(2, 16));
+    const bool fault = uni(0, 4) == 0;
+    setenv("LBF_WORKERS_PER_DEVICE", std::to_string(workers).c_str(), 1);
+    setenv("LBF_SLOTS", std::to_string(slots).c_str(), 1);
+    setenv("LBF_SLOT_MB", std::to_string(slot_mb).c_str(), 1);
+    setenv("LBF_TEST_FAULT_GROUP", fault ? std::to_string(uni(0, 3)).c_str() : "-1", 1);
+    setenv("LBF_TEST_FAULT_WORKER", std::to_string(uni(0, workers - 1)).c_str(), 1);
+    lbf_ctx* ctx = nullptr;
+    if (lbf_ctx_create(1, &ctx) != LBF_OK) {
+      std::fprintf(stderr, "lbf_ctx_create: %s\n", lbf_last_error());
+      return 2;
+    }
+    for (int job = 0; job < 3; ++job) {
+      // ---- batch ----
+      const uint64_t buf_len = uni(1, 12) << 20;
+      std::vector<uint8_t> buf(buf_len);
+      oracle_synth_fill_mt(buf.data(), buf_len, rng(), 0, 4);
+      const uint64_t n = uni(0, 1) ? uni(0, 40) : uni(0, 1500);
+      std::vector<uint64_t> off(n);
+      std::vector<uint32_t> size(n);
+      for (uint64_t i = 0; i < n; ++i) {
+        const int kind = (int)uni(0, 9);
+        uint64_t s = kind == 0 ? uni(0, 130) : kind == 1 ? uni(1, 3) << 20 : uni(0, kind < 5 ? 70000 : 300000);
+        s = std::min<uint64_t>(s, buf_len);
+        size[i] = (uint32_t)s;
+        off[i] = uni(0, buf_len - s);
+        if (uni(0, 2) == 0) off[i] &= ~63ull;
+      }
+      std::vector<uint8_t> want(20 * n), got(20 * n, 0xEE);
+      for (uint64_t i = 0; i < n; ++i) oracle_sha1(buf.data() + off[i], size[i], &want[20 * i]);
+      ++cases;
+      int rc = lbf_sha1_batch(ctx, buf.data(), buf_len, off.data(), size.data(), n, got.data(), LBF_HOST_PTR);
+      if (rc == LBF_ERR_HIP && strstr(lbf_last_error(), "injected fault")) {
+        ++faults;  // one-shot: the same job must now succeed on the same context
+        rc = lbf_sha1_batch(ctx, buf.data(), buf_len, off.data(), size.data(), n, got.data(), LBF_HOST_PTR);
+      }
+      CHECK(rc == LBF_OK, "hash rc %d: %s", rc, lbf_last_error());
+      for (uint64_t i = 0; i < n && rc == LBF_OK; ++i)
+        CHECK(memcmp(&got[20 * i], &want[20 * i], 20) == 0, "hash chunk %lu size %u off %lu", (unsigned long)i,
+              size[i], (unsigned long)off[i]);
+      chunks_checked += (long)n;
+      // verify with some expected digests corrupted
+      std::vector<uint8_t> exp = want, ver(n, 7);
+      std::vector<uint8_t> bad(n, 0);
+      for (uint64_t i = 0; i < n; ++i)
+        if (uni(0, 7) == 0) {
+          exp[20 * i + uni(0, 19)] ^= (uint8_t)(1u << uni(0, 7));
+          bad[i] = 1;
+        }
+      rc = lbf_verify_batch(ctx, buf.data(), buf_len, off.data(), size.data(), n, exp.data(), ver.data(), LBF_HOST_PTR);
+      if (rc == LBF_ERR_HIP && strstr(lbf_last_error(), "injected fault")) {
+        ++faults;
+        rc = lbf_verify_batch(ctx, buf.data(), buf_len, off.data(), size.data(), n, exp.data(), ver.data(),
+                              LBF_HOST_PTR);
+      }
+      CHECK(rc == LBF_OK, "verify rc %d: %s", rc, lbf_last_error());
+      for (uint64_t i = 0; i < n && rc == LBF_OK; ++i) CHECK(ver[i] == (bad[i] ? 0 : 1), "verdict %lu", (unsigned long)i);
+      // the same chunks from a file, truncated in half of the cases
+      const uint64_t keep = uni(0, 1) ? buf_len : uni(0, buf_len);
+      const int fd = open(path.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
+      CHECK(fd >= 0 && write(fd, buf.data(), keep) == (ssize_t)keep, "write %s", path.c_str());
+      close(fd);
+      std::vector<uint8_t> fver(n, 7);
+      rc = lbf_file_ranges(ctx, path.c_str(), off.data(), size.data(), n, want.data(), fver.data());
+      if (rc == LBF_ERR_HIP && strstr(lbf_last_error(), "injected fault")) {
+        ++faults;
+        rc = lbf_file_ranges(ctx, path.c_str(), off.data(), size.data(), n, want.data(), fver.data());
+      }
+      CHECK(rc == LBF_OK, "file verify rc %d: %s", rc, lbf_last_error());
+      bool all_present = true;
+      for (uint64_t i = 0; i < n && rc == LBF_OK; ++i) {
+        const bool present = size[i] == 0 || off[i] + size[i] <= keep;
+        all_present = all_present && present;
+        CHECK(fver[i] == (present ? 1 : 0), "file verdict %lu", (unsigned long)i);
+      }
+      std::vector<uint8_t> fdig(20 * n, 0);
+      rc = lbf_file_ranges(ctx, path.c_str(), off.data(), size.data(), n, nullptr, fdig.data());
+      if (rc == LBF_ERR_HIP && strstr(lbf_last_error(), "injected fault")) {
+        ++faults;
+        rc = lbf_file_ranges(ctx, path.c_str(), off.data(), size.data(), n, nullptr, fdig.data());
+      }
+      if (all_present) {
+        CHECK(rc == LBF_OK, "file hash rc %d: %s", rc, lbf_last_error());
+        CHECK(n == 0 || memcmp(fdig.data(), want.data(), 20 * n) == 0, "file digests");
+      } else {
+        CHECK(rc == LBF_ERR_IO, "file hash of a truncated file rc %d: %s", rc, lbf_last_error());
+      }
+    }
+    lbf_ctx_destroy(ctx);
+  }
+  unlink(path.c_str());
+  std::printf("asan_capi %s: %ld cases, %ld chunks, %ld injected faults, seed %lu\n", g_fail ? "FAIL" : "OK", cases,
+              chunks_checked, faults, (unsigned long)seed);
+  return g_fail ? 1 : 0;
+}
