@@ -146,5 +146,10 @@ int main(int argc, char** argv) {
   unlink(path.c_str());
   std::printf("asan_capi %s: %ld cases, %ld chunks, %ld injected faults, seed %lu\n", g_fail ? "FAIL" : "OK", cases,
               chunks_checked, faults, (unsigned long)seed);
-  return g_fail ? 1 : 0;
+  std::fflush(stdout);
+  // Skip static destructors: the HIP runtime's own teardown (libamdhip64
+  // __cxa_finalize) can trip ASan's device-allocator CHECK
+  // (sanitizer_allocator_device.h "dev_runtime_unloaded_") after ROCr has
+  // unloaded -- a runtime/ASan interaction at exit, not a finding in this code.
+  _exit(g_fail ? 1 : 0);
 }
