@@ -20,6 +20,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cctype>
 #include <cstdio>
 #include <cstdlib>
@@ -469,6 +470,55 @@ struct Source {
   }
 };
 
+// A run: consecutive descriptors whose byte ranges follow each other in the
+// source, staged with one copy.  `dst` is its position in the slot's data
+// area (same 16-byte phase as `src`); `avail` is how much of it was read.
+struct Run {
+  uint64_t src = 0, len = 0, dst = 0, avail = 0;
+};
+
+// Copy every run of a group into the slot's data area.  Runs are cut into
+// pieces of at most `step` bytes that up to `threads` threads (bound to the
+// staging's NUMA node) pull from a shared index, so a group of many small
+// scattered chunks copies in parallel as well as one long contiguous run does.
+void read_runs(const Source& src, std::vector<Run>& runs, uint8_t* data, const std::vector<int>& cpus) {
+  constexpr uint64_t kMinPart = 8ull << 20;
+  uint64_t total = 0;
+  for (const Run& r : runs) total += r.len;
+  const uint64_t parts = std::min<uint64_t>(src.threads, total / kMinPart);
+  if (parts <= 1) {
+    for (Run& r : runs) r.avail = src.read_serial(data + r.dst, r.src, r.len);
+    return;
+  }
+  const uint64_t step = ((total + parts - 1) / parts + 4095) & ~4095ull;
+  struct Piece {
+    size_t run;
+    uint64_t at, len, got;
+  };
+  std::vector<Piece> pieces;
+  for (size_t k = 0; k < runs.size(); ++k)
+    for (uint64_t a = 0; a < runs[k].len; a += step) pieces.push_back({k, a, std::min(step, runs[k].len - a), 0});
+  std::atomic<size_t> next{0};
+  std::vector<std::thread> th;
+  for (uint64_t t = 0; t < parts; ++t)
+    th.emplace_back([&] {
+      bind_thread(cpus);
+      for (size_t q; (q = next++) < pieces.size();) {
+        Piece& pc = pieces[q];
+        pc.got = src.read_serial(data + runs[pc.run].dst + pc.at, runs[pc.run].src + pc.at, pc.len);
+      }
+    });
+  for (auto& t : th) t.join();
+  // a run's readable prefix: its pieces in order up to the first short one
+  std::vector<bool> short_seen(runs.size(), false);
+  for (Run& r : runs) r.avail = 0;
+  for (const Piece& pc : pieces) {
+    if (short_seen[pc.run]) continue;
+    runs[pc.run].avail += pc.got;
+    if (pc.got < pc.len) short_seen[pc.run] = true;
+  }
+}
+
 struct Job {
   Source src;
   const uint64_t* offsets;
@@ -478,19 +528,33 @@ struct Job {
   uint8_t* verdicts;        // verify mode output
 };
 
-// Copy finished results of a slot's group to the caller's arrays.  Chunks that
-// were not fully readable: verdict 0 (verify) or an LBF_ERR_IO (hash).
-int finalize(const Job& job, Slot& s) {
+// The order a worker stages its descriptors in: positions [begin, end) map to
+// job indices through `perm` (empty = identity, the common sorted case).
+struct Order {
+  uint64_t begin = 0;
+  std::vector<uint64_t> perm;
+  uint64_t operator()(uint64_t pos) const { return perm.empty() ? pos : perm[pos - begin]; }
+};
+
+// Copy finished results of a slot's group (positions [g_begin, g_end)) to the
+// caller's arrays.  Chunks that were not fully readable: verdict 0 (verify) or
+// an LBF_ERR_IO (hash).
+int finalize(const Job& job, const Order& order, Slot& s) {
   if (!s.pending) return LBF_OK;
   s.pending = false;
   const uint64_t cnt = s.g_end - s.g_begin;
   if (job.expected) {
-    for (uint64_t k = 0; k < cnt; ++k) job.verdicts[s.g_begin + k] = s.h_out[k] & s.ok[k];
+    for (uint64_t k = 0; k < cnt; ++k) job.verdicts[order(s.g_begin + k)] = s.h_out[k] & s.ok[k];
     return LBF_OK;
   }
   for (uint64_t k = 0; k < cnt; ++k)
-    if (!s.ok[k]) return fail(LBF_ERR_IO, "chunk " + std::to_string(s.g_begin + k) + " could not be read in full");
-  memcpy(job.digests + 20 * s.g_begin, s.h_out, cnt * 20);
+    if (!s.ok[k])
+      return fail(LBF_ERR_IO, "chunk " + std::to_string(order(s.g_begin + k)) + " could not be read in full");
+  if (order.perm.empty()) {
+    memcpy(job.digests + 20 * s.g_begin, s.h_out, cnt * 20);
+  } else {
+    for (uint64_t k = 0; k < cnt; ++k) memcpy(job.digests + 20 * order(s.g_begin + k), s.h_out + 20 * k, 20);
+  }
   return LBF_OK;
 }
 
@@ -547,23 +611,61 @@ int run_oversize(Worker& w, const Job& job, uint64_t i) {
 // Every exit, error or not, passes the drain at the end: each slot's stream is
 // synchronized and its pending group cleared, so nothing is still in flight
 // and no stale group can be finalized into the next job's arrays.
+// Descriptors closer than this to the end of the current run join it: the gap
+// is copied along (cheaper than another copy); the 16-byte padding between
+// ReadVerifiedChunks' arena slots is the common case.
+constexpr uint64_t kJoinGap = 4096;
+
+// Process descriptors [begin, end) on one worker.  They are staged in source
+// order: sorted by offset (a stable permutation, skipped when the table is
+// already sorted, as every file-order table is).  A group is a run of
+// positions whose bytes fit a slot, packed as runs: a descriptor that starts
+// inside, or within kJoinGap of, the current run extends it (a contiguous
+// table is one run and one copy; overlapping chunks share their bytes); any
+// other starts a new run at the next free position with its 16-byte phase.
+// So a group holds as many chunks as their bytes fit, wherever they lie in
+// the source.  (Round 1 grouped by the covering range of consecutive
+// descriptors in caller order, which collapsed to one or two chunks per group
+// for a scattered table: 8.5 s for 3,000 random chunks of a 160 MiB buffer,
+// tools/staging_probe.py.)  One H2D per group, one kernel, one D2H; the host
+// stages group g+1 while the GPU works on the groups before it.
+//
+// Every exit, error or not, passes the drain at the end: each slot's stream is
+// synchronized and its pending group cleared, so nothing is still in flight
+// and no stale group can be finalized into the next job's arrays.
 int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
   LBF_HIP_TRY(hipSetDevice(w.device));
+  Order order;
+  order.begin = begin;
+  for (uint64_t k = begin + 1; k < end; ++k)
+    if (job.offsets[k] < job.offsets[k - 1]) {
+      order.perm.resize(end - begin);
+      for (uint64_t q = begin; q < end; ++q) order.perm[q - begin] = q;
+      std::stable_sort(order.perm.begin(), order.perm.end(),
+                       [&](uint64_t x, uint64_t y) { return job.offsets[x] < job.offsets[y]; });
+      break;
+    }
   {
-    // Staging sized to the byte range this worker covers: a quarter of it per
-    // slot once it exceeds kSplitMin, so a mid-sized job still runs as several
-    // groups whose copies, H2Ds and kernels overlap; never below the largest
-    // chunk that fits a slot, and capped at slot_max.
+    // Staging sized to the bytes this worker stages (the union of its runs):
+    // a quarter of them per slot once they exceed kSplitMin, so a mid-sized job
+    // still runs as several groups whose copies, H2Ds and kernels overlap;
+    // never below the largest chunk that fits a slot, and capped at slot_max.
     constexpr uint64_t kSplitMin = 32ull << 20;
-    uint64_t lo = UINT64_MAX, hi = 0, largest = 0;
-    for (uint64_t k = begin; k < end; ++k)
-      if ((uint64_t)job.sizes[k] + 15 <= w.slot_max) {
-        lo = std::min(lo, job.offsets[k]);
-        hi = std::max(hi, job.offsets[k] + job.sizes[k]);
-        largest = std::max<uint64_t>(largest, job.sizes[k]);
+    uint64_t bytes = 0, largest = 0, run_end = 0;
+    bool open = false;
+    for (uint64_t q = begin; q < end; ++q) {
+      const uint64_t k = order(q), o = job.offsets[k], sz = job.sizes[k];
+      if (sz == 0 || sz + 15 > w.slot_max) continue;
+      largest = std::max(largest, sz);
+      if (open && o <= run_end + kJoinGap) {
+        if (o + sz > run_end) bytes += o + sz - run_end, run_end = o + sz;
+      } else {
+        bytes += sz;
+        run_end = o + sz;
+        open = true;
       }
-    const uint64_t span = hi > lo ? hi - lo : 0;
-    const uint64_t per = span <= kSplitMin ? span : std::max({kSplitMin, (span + 3) / 4, largest});
+    }
+    const uint64_t per = bytes <= kSplitMin ? bytes : std::max({kSplitMin, (bytes + 3) / 4, largest});
     if (end > begin)
       if (int rc = ensure_slot_bytes(w, std::min(per, w.slot_max) + 16)) return rc;  // nothing pending yet
   }
@@ -571,34 +673,53 @@ int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
   uint64_t i = begin;
   int rc = LBF_OK;
   long group = 0;
+  std::vector<Run> runs;
+  std::vector<uint32_t> run_of;  // per position of the group: its run, or UINT32_MAX for an empty chunk
   auto hip_ok = [&rc](hipError_t e, const char* what) {
     if (e == hipSuccess) return true;
     rc = hip_fail(e, what);
     return false;
   };
   while (i < end && rc == LBF_OK) {
-    if ((uint64_t)job.sizes[i] + 15 > w.slot_bytes) {
+    if ((uint64_t)job.sizes[order(i)] + 15 > w.slot_bytes) {
       for (Slot& s : w.slot) {
         if (!hip_ok(hipStreamSynchronize(s.stream), "hipStreamSynchronize")) break;
-        if ((rc = finalize(job, s))) break;
+        if ((rc = finalize(job, order, s))) break;
       }
-      if (rc == LBF_OK) rc = run_oversize(w, job, i);
+      if (rc == LBF_OK) rc = run_oversize(w, job, order(i));
       ++i;
       continue;
     }
-    uint64_t lo = job.offsets[i], hi = lo + job.sizes[i];
-    uint64_t j = i + 1;
+    // group [i, j) of positions, packed as runs
+    runs.clear();
+    run_of.clear();
+    uint64_t cursor = 0, j = i;
     while (j < end && j - i < w.desc_cap) {
-      const uint64_t o = job.offsets[j], e = o + job.sizes[j];
-      const uint64_t nlo = std::min(lo, o), nhi = std::max(hi, e);
-      if (nhi - nlo + 15 > w.slot_bytes) break;
-      lo = nlo;
-      hi = nhi;
+      const uint64_t k = order(j), o = job.offsets[k], sz = job.sizes[k];
+      if (sz == 0) {  // empty chunks take no bytes
+        run_of.push_back(UINT32_MAX);
+        ++j;
+        continue;
+      }
+      if (sz + 15 > w.slot_bytes) break;  // oversize: the next group starts with it
+      Run* r = runs.empty() ? nullptr : &runs.back();
+      if (r && o >= r->src && o <= r->src + r->len + kJoinGap) {
+        const uint64_t new_len = std::max(r->len, o + sz - r->src);
+        if (r->dst + new_len > w.slot_bytes) break;
+        r->len = new_len;
+        cursor = r->dst + new_len;
+      } else {
+        const uint64_t p = cursor + ((o - cursor) & 15u);
+        if (p + sz > w.slot_bytes) break;
+        runs.push_back(Run{o, sz, p, 0});
+        cursor = p + sz;
+      }
+      run_of.push_back((uint32_t)(runs.size() - 1));
       ++j;
     }
     Slot& s = w.slot[cur];
     if (!hip_ok(hipStreamSynchronize(s.stream), "hipStreamSynchronize")) break;
-    if ((rc = finalize(job, s))) break;
+    if ((rc = finalize(job, order, s))) break;
     if (group++ == w.fault_group) {
       w.fault_group = -1;
       rc = fail(LBF_ERR_HIP, "injected fault (LBF_TEST_FAULT_GROUP) at group " + std::to_string(group - 1));
@@ -609,24 +730,20 @@ int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
     uint64_t* h_off = reinterpret_cast<uint64_t*>(s.h_buf);
     uint32_t* h_size = reinterpret_cast<uint32_t*>(s.h_buf + 8 * cnt);
     uint8_t* h_exp = s.h_buf + 12 * cnt;
-    // The covered range [lo, hi) lands at data + (lo % 16) so each chunk keeps
-    // its offset's 16-byte phase (aligned chunks take the vector-load path on
-    // the device).
-    const uint64_t shift = lo & 15u;
-    const uint64_t avail = job.src.read(s.h_buf + hdr + shift, lo, hi - lo, w.cpus);
-    for (uint64_t k = 0; k < cnt; ++k) {
-      const uint64_t o = job.offsets[i + k], sz = job.sizes[i + k];
+    read_runs(job.src, runs, s.h_buf + hdr, w.cpus);
+    for (uint64_t q = 0; q < cnt; ++q) {
+      const uint64_t k = order(i + q), o = job.offsets[k], sz = job.sizes[k];
+      const uint32_t r = run_of[q];
       // An empty chunk is always readable, wherever it lies: the reference's
       // fseek succeeds past EOF and fread of 0 bytes returns 0 (Flood.cpp:259-275).
-      s.ok[k] = (sz == 0 || o + sz <= lo + avail) ? 1 : 0;
-      // Unreadable chunks must not be hashed from stale slot bytes past
-      // `avail`: they get size 0 on the device (their result is discarded).
-      h_off[k] = s.ok[k] ? o - lo + shift : 0;
-      h_size[k] = s.ok[k] ? (uint32_t)sz : 0;
+      // Unreadable chunks must not be hashed from stale slot bytes: they get
+      // size 0 on the device (their result is discarded).
+      s.ok[q] = (r == UINT32_MAX || o + sz <= runs[r].src + runs[r].avail) ? 1 : 0;
+      h_off[q] = (r != UINT32_MAX && s.ok[q]) ? runs[r].dst + (o - runs[r].src) : 0;
+      h_size[q] = s.ok[q] ? (uint32_t)sz : 0;
+      if (job.expected) memcpy(h_exp + 20 * q, job.expected + 20 * k, 20);
     }
-    if (job.expected) memcpy(h_exp, job.expected + 20 * i, cnt * 20);
-    if (!hip_ok(hipMemcpyAsync(s.d_buf, s.h_buf, hdr + shift + avail, hipMemcpyHostToDevice, s.stream),
-                "hipMemcpyAsync(H2D)"))
+    if (!hip_ok(hipMemcpyAsync(s.d_buf, s.h_buf, hdr + cursor, hipMemcpyHostToDevice, s.stream), "hipMemcpyAsync(H2D)"))
       break;
     const uint64_t* d_off = reinterpret_cast<const uint64_t*>(s.d_buf);
     const uint32_t* d_size = reinterpret_cast<const uint32_t*>(s.d_buf + 8 * cnt);
@@ -646,7 +763,7 @@ int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
   for (Slot& s : w.slot) {
     const hipError_t e = hipStreamSynchronize(s.stream);
     if (e != hipSuccess && rc == LBF_OK) rc = hip_fail(e, "hipStreamSynchronize");
-    if (rc == LBF_OK) rc = finalize(job, s);
+    if (rc == LBF_OK) rc = finalize(job, order, s);
     s.pending = false;
   }
   return rc;
