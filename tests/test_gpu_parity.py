@@ -327,3 +327,26 @@ def test_more_chunks_than_one_group_holds(hasher, oracle):
     flips = [0, 65535, 65536, 131072, n - 1]
     exp[flips, 11] ^= 0x80
     assert np.flatnonzero(~hasher.verify_chunks(buf, offs, sizes, exp)).tolist() == flips
+
+
+def test_unsorted_overlapping_duplicate_table(hasher, oracle):
+    """The staging sorts descriptors by offset and packs them as joined runs
+    (lbf_capi.cpp worker_run); results must land at the caller's indices:
+    a descending table, exact duplicates, chunks nested in others, chunks far
+    apart, and empty chunks anywhere, in hash and verify mode."""
+    buf = oracle.synth(71, 0, 64 << 20, nthreads=8)
+    rng = np.random.default_rng(71)
+    offs = list(range((60 << 20), 0, -(3 << 20)))          # descending, 3 MiB apart
+    sizes = [1 << 20] * len(offs)
+    offs += [5, 5, 5 + 4096, 1000, 63 << 20]                   # duplicates, nested, far
+    sizes += [70000, 70000, 100, 0, (1 << 20) - 1]
+    offs += [int(x) for x in rng.integers(0, 60 << 20, 500)]  # random, overlapping
+    sizes += [int(x) for x in rng.integers(0, 300000, 500)]
+    offs = np.array(offs, dtype=np.uint64)
+    sizes = np.array(sizes, dtype=np.uint32)
+    want = oracle.sha1_batch(buf, offs, sizes, nthreads=8)
+    assert np.array_equal(hasher.hash_chunks(buf, offs, sizes), want)
+    exp = want.copy()
+    flips = [0, 7, 21, 22, 300, len(offs) - 1]
+    exp[flips, 19] ^= 1
+    assert np.flatnonzero(~hasher.verify_chunks(buf, offs, sizes, exp)).tolist() == flips
