@@ -55,6 +55,8 @@ _SIGS = {
     "lbf_sha1_one": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_uint32, _c.c_void_p]),
     "lbf_file_ranges": (_c.c_int, [_c.c_void_p, _c.c_char_p, _c.c_void_p, _c.c_void_p, _c.c_uint64,
                                    _c.c_void_p, _c.c_void_p]),
+    "lbf_files_ranges": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_uint32, _c.c_void_p, _c.c_void_p, _c.c_void_p,
+                                    _c.c_uint64, _c.c_void_p, _c.c_void_p]),
     "lbf_b64_27": (None, [_c.c_void_p, _c.c_char_p]),
     "lbf_b64_27_decode": (_c.c_int, [_c.c_char_p, _c.c_size_t, _c.c_void_p]),
     "lbf_sha1_launch": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_uint64, _c.c_void_p,

@@ -414,59 +414,31 @@ unsigned copy_threads() {
   return n;
 }
 
-// Where a job's bytes come from: caller memory (bounds-checked up front) or a
-// file read with pread.  read() returns the bytes actually available.
+// Where a job's bytes come from: caller memory (bounds-checked up front) or
+// files read with pread (one descriptor table over several files: each
+// descriptor names its file).  read_serial() returns the bytes available.
 struct Source {
   const uint8_t* base = nullptr;  // memory source
   uint64_t base_len = 0;
-  int fd = -1;                    // file source
+  std::vector<int> fds;           // file source: one fd per file, -1 = could not be opened
   unsigned threads = copy_threads();  // staging copy threads
 
-  uint64_t read_serial(uint8_t* dst, uint64_t off, uint64_t len) const {
-    if (fd < 0) {
+  bool from_files() const { return !fds.empty(); }
+  bool exists(uint32_t file) const { return !from_files() || fds[file] >= 0; }
+
+  uint64_t read_serial(uint8_t* dst, uint32_t file, uint64_t off, uint64_t len) const {
+    if (!from_files()) {
       memcpy(dst, base + off, len);
       return len;
     }
+    const int fd = fds[file];
     uint64_t got = 0;
-    while (got < len) {
+    while (fd >= 0 && got < len) {
       const ssize_t r = pread(fd, dst + got, len - got, (off_t)(off + got));
       if (r <= 0) break;  // EOF or error: the rest is unavailable
       got += (uint64_t)r;
     }
     return got;
-  }
-
-  // A single host thread copies ~17 GiB/s into pinned memory, a third of what
-  // PCIe Gen5 moves, so large ranges are split over `threads` contiguous
-  // parts, each on a thread bound to `cpus` (the staging's NUMA node).
-  // Returns the length of the readable prefix, as read_serial does.
-  uint64_t read(uint8_t* dst, uint64_t off, uint64_t len, const std::vector<int>& cpus) const {
-    constexpr uint64_t kMinPart = 8ull << 20;
-    const uint64_t parts = std::min<uint64_t>(threads, len / kMinPart);
-    if (parts <= 1) return read_serial(dst, off, len);
-    // ceil(len / parts), rounded up to a page: parts * step must cover len.
-    // (Rounding floor(len / parts) instead left the last len % parts bytes
-    // uncopied whenever floor(len / parts) was already a page multiple; found
-    // by tools/fuzz_gpu.py, regression test test_staging_split_covers_tail.)
-    const uint64_t step = ((len + parts - 1) / parts + 4095) & ~4095ull;
-    std::vector<uint64_t> got(parts, 0), want(parts, 0);
-    std::vector<std::thread> th;
-    for (uint64_t p = 0; p < parts; ++p) {
-      const uint64_t a = p * step;
-      if (a >= len) break;
-      want[p] = std::min(step, len - a);
-      th.emplace_back([&, p, a] {
-        bind_thread(cpus);
-        got[p] = read_serial(dst + a, off + a, want[p]);
-      });
-    }
-    for (auto& t : th) t.join();
-    uint64_t total = 0;
-    for (uint64_t p = 0; p < parts; ++p) {
-      total += got[p];
-      if (got[p] < want[p]) break;
-    }
-    return total;
   }
 };
 
@@ -475,19 +447,25 @@ struct Source {
 // area (same 16-byte phase as `src`); `avail` is how much of it was read.
 struct Run {
   uint64_t src = 0, len = 0, dst = 0, avail = 0;
+  uint32_t file = 0;
 };
 
-// Copy every run of a group into the slot's data area.  Runs are cut into
-// pieces of at most `step` bytes that up to `threads` threads (bound to the
-// staging's NUMA node) pull from a shared index, so a group of many small
-// scattered chunks copies in parallel as well as one long contiguous run does.
+// Copy every run of a group into the slot's data area.  A single host thread
+// copies ~17 GiB/s into pinned memory, a third of what PCIe Gen5 moves, so
+// runs are cut into pieces of at most `step` bytes (≥ 8 MiB of work per
+// thread; `step` rounded up to a page) that up to `threads` threads, bound to
+// the staging's NUMA node, pull from a shared index: one long contiguous run
+// and many small scattered ones copy in parallel alike.  (The ceil(total /
+// parts) step must cover everything: rounding floor(len / parts) once left the
+// last bytes of a range uncopied, tools/fuzz_gpu.py seed 23006099, pinned by
+// test_staging_split_covers_tail.)
 void read_runs(const Source& src, std::vector<Run>& runs, uint8_t* data, const std::vector<int>& cpus) {
   constexpr uint64_t kMinPart = 8ull << 20;
   uint64_t total = 0;
   for (const Run& r : runs) total += r.len;
   const uint64_t parts = std::min<uint64_t>(src.threads, total / kMinPart);
   if (parts <= 1) {
-    for (Run& r : runs) r.avail = src.read_serial(data + r.dst, r.src, r.len);
+    for (Run& r : runs) r.avail = src.read_serial(data + r.dst, r.file, r.src, r.len);
     return;
   }
   const uint64_t step = ((total + parts - 1) / parts + 4095) & ~4095ull;
@@ -505,7 +483,7 @@ void read_runs(const Source& src, std::vector<Run>& runs, uint8_t* data, const s
       bind_thread(cpus);
       for (size_t q; (q = next++) < pieces.size();) {
         Piece& pc = pieces[q];
-        pc.got = src.read_serial(data + runs[pc.run].dst + pc.at, runs[pc.run].src + pc.at, pc.len);
+        pc.got = src.read_serial(data + runs[pc.run].dst + pc.at, runs[pc.run].file, runs[pc.run].src + pc.at, pc.len);
       }
     });
   for (auto& t : th) t.join();
@@ -521,11 +499,13 @@ void read_runs(const Source& src, std::vector<Run>& runs, uint8_t* data, const s
 
 struct Job {
   Source src;
+  const uint32_t* file_of = nullptr;  // file of each descriptor (null: all in file / buffer 0)
   const uint64_t* offsets;
   const uint32_t* sizes;
   const uint8_t* expected;  // null => hash mode
   uint8_t* digests;         // hash mode output
   uint8_t* verdicts;        // verify mode output
+  uint32_t file(uint64_t k) const { return file_of ? file_of[k] : 0; }
 };
 
 // The order a worker stages its descriptors in: positions [begin, end) map to
@@ -564,7 +544,9 @@ int run_oversize(Worker& w, const Job& job, uint64_t i) {
   LBF_HIP_TRY(hipStreamSynchronize(s.stream));
   const uint32_t sz = job.sizes[i];
   std::vector<uint8_t> host(sz ? sz : 1);
-  const bool ok = job.src.read(host.data(), job.offsets[i], sz, w.cpus) == sz;
+  std::vector<Run> one{Run{job.offsets[i], sz, 0, 0, job.file(i)}};
+  read_runs(job.src, one, host.data(), w.cpus);
+  const bool ok = one[0].avail == sz && job.src.exists(job.file(i));
   if (!ok) {
     if (job.expected) {
       job.verdicts[i] = 0;
@@ -637,12 +619,15 @@ int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
   LBF_HIP_TRY(hipSetDevice(w.device));
   Order order;
   order.begin = begin;
+  auto before = [&](uint64_t x, uint64_t y) {  // source order: file, then offset
+    const uint32_t fx = job.file(x), fy = job.file(y);
+    return fx != fy ? fx < fy : job.offsets[x] < job.offsets[y];
+  };
   for (uint64_t k = begin + 1; k < end; ++k)
-    if (job.offsets[k] < job.offsets[k - 1]) {
+    if (before(k, k - 1)) {
       order.perm.resize(end - begin);
       for (uint64_t q = begin; q < end; ++q) order.perm[q - begin] = q;
-      std::stable_sort(order.perm.begin(), order.perm.end(),
-                       [&](uint64_t x, uint64_t y) { return job.offsets[x] < job.offsets[y]; });
+      std::stable_sort(order.perm.begin(), order.perm.end(), before);
       break;
     }
   {
@@ -652,16 +637,18 @@ int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
     // never below the largest chunk that fits a slot, and capped at slot_max.
     constexpr uint64_t kSplitMin = 32ull << 20;
     uint64_t bytes = 0, largest = 0, run_end = 0;
+    uint32_t run_file = 0;
     bool open = false;
     for (uint64_t q = begin; q < end; ++q) {
       const uint64_t k = order(q), o = job.offsets[k], sz = job.sizes[k];
       if (sz == 0 || sz + 15 > w.slot_max) continue;
       largest = std::max(largest, sz);
-      if (open && o <= run_end + kJoinGap) {
+      if (open && job.file(k) == run_file && o <= run_end + kJoinGap) {
         if (o + sz > run_end) bytes += o + sz - run_end, run_end = o + sz;
       } else {
         bytes += sz;
         run_end = o + sz;
+        run_file = job.file(k);
         open = true;
       }
     }
@@ -703,7 +690,7 @@ int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
       }
       if (sz + 15 > w.slot_bytes) break;  // oversize: the next group starts with it
       Run* r = runs.empty() ? nullptr : &runs.back();
-      if (r && o >= r->src && o <= r->src + r->len + kJoinGap) {
+      if (r && r->file == job.file(k) && o >= r->src && o <= r->src + r->len + kJoinGap) {
         const uint64_t new_len = std::max(r->len, o + sz - r->src);
         if (r->dst + new_len > w.slot_bytes) break;
         r->len = new_len;
@@ -711,7 +698,7 @@ int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
       } else {
         const uint64_t p = cursor + ((o - cursor) & 15u);
         if (p + sz > w.slot_bytes) break;
-        runs.push_back(Run{o, sz, p, 0});
+        runs.push_back(Run{o, sz, p, 0, job.file(k)});
         cursor = p + sz;
       }
       run_of.push_back((uint32_t)(runs.size() - 1));
@@ -734,11 +721,12 @@ int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
     for (uint64_t q = 0; q < cnt; ++q) {
       const uint64_t k = order(i + q), o = job.offsets[k], sz = job.sizes[k];
       const uint32_t r = run_of[q];
-      // An empty chunk is always readable, wherever it lies: the reference's
-      // fseek succeeds past EOF and fread of 0 bytes returns 0 (Flood.cpp:259-275).
-      // Unreadable chunks must not be hashed from stale slot bytes: they get
-      // size 0 on the device (their result is discarded).
-      s.ok[q] = (r == UINT32_MAX || o + sz <= runs[r].src + runs[r].avail) ? 1 : 0;
+      // An empty chunk of an existing file is always readable, wherever it
+      // lies: the reference's fseek succeeds past EOF and fread of 0 bytes
+      // returns 0 (Flood.cpp:259-275); a file that cannot be opened leaves every
+      // chunk '0' (Flood.cpp:257).  Unreadable chunks must not be hashed from
+      // stale slot bytes: they get size 0 on the device (result discarded).
+      s.ok[q] = (r == UINT32_MAX ? job.src.exists(job.file(k)) : o + sz <= runs[r].src + runs[r].avail) ? 1 : 0;
       h_off[q] = (r != UINT32_MAX && s.ok[q]) ? runs[r].dst + (o - runs[r].src) : 0;
       h_size[q] = s.ok[q] ? (uint32_t)sz : 0;
       if (job.expected) memcpy(h_exp + 20 * q, job.expected + 20 * k, 20);
@@ -914,28 +902,50 @@ extern "C" int lbf_verify_batch(lbf_ctx* ctx, const uint8_t* base, uint64_t base
   return run_job(ctx, job, n);
 }
 
-extern "C" int lbf_file_ranges(lbf_ctx* ctx, const char* path, const uint64_t* offsets, const uint32_t* sizes,
-                               uint64_t n, const uint8_t* expected, uint8_t* out) {
-  if (!ctx || !path) return fail(LBF_ERR_INVALID, "null context/path");
+extern "C" int lbf_files_ranges(lbf_ctx* ctx, const char* const* paths, uint32_t n_files, const uint32_t* file_of,
+                                const uint64_t* offsets, const uint32_t* sizes, uint64_t n, const uint8_t* expected,
+                                uint8_t* out) {
+  if (!ctx || !paths || n_files == 0) return fail(LBF_ERR_INVALID, "null context/paths or no file");
   if (n == 0) return LBF_OK;
-  if (!offsets || !sizes || !out) return fail(LBF_ERR_INVALID, "null argument");
-  const int fd = open(path, O_RDONLY | O_CLOEXEC);
-  if (fd < 0) {
-    if (!expected) return fail(LBF_ERR_IO, std::string("cannot open ") + path);
-    memset(out, 0, n);  // Flood.cpp:257: no file -> every chunk stays '0'
+  if (!offsets || !sizes || !out || (n_files > 1 && !file_of)) return fail(LBF_ERR_INVALID, "null argument");
+  if (file_of)
+    for (uint64_t i = 0; i < n; ++i)
+      if (file_of[i] >= n_files) return fail(LBF_ERR_INVALID, "chunk " + std::to_string(i) + " names no file");
+  Job job{};
+  job.src.fds.assign(n_files, -1);
+  struct Closer {  // every opened file is closed on every path
+    std::vector<int>& fds;
+    ~Closer() {
+      for (int fd : fds)
+        if (fd >= 0) close(fd);
+    }
+  } closer{job.src.fds};
+  for (uint32_t f = 0; f < n_files; ++f) {
+    if (!paths[f]) return fail(LBF_ERR_INVALID, "null path");
+    const int fd = open(paths[f], O_RDONLY | O_CLOEXEC);
+    // hash mode needs every file; verify mode leaves a missing file's chunks
+    // '0' (Flood.cpp:257)
+    if (fd < 0 && !expected) return fail(LBF_ERR_IO, std::string("cannot open ") + paths[f]);
+    if (fd >= 0) posix_fadvise(fd, 0, 0, POSIX_FADV_SEQUENTIAL);
+    job.src.fds[f] = fd;
+  }
+  if (std::all_of(job.src.fds.begin(), job.src.fds.end(), [](int fd) { return fd < 0; })) {
+    memset(out, 0, n);  // verify mode, no file there: every chunk stays '0'
     return LBF_OK;
   }
-  posix_fadvise(fd, 0, 0, POSIX_FADV_SEQUENTIAL);
-  Job job{};
-  job.src.fd = fd;
+  job.file_of = file_of;
   job.offsets = offsets;
   job.sizes = sizes;
   job.expected = expected;
   if (expected) job.verdicts = out;
   else job.digests = out;
-  const int rc = run_job(ctx, job, n);
-  close(fd);
-  return rc;
+  return run_job(ctx, job, n);
+}
+
+extern "C" int lbf_file_ranges(lbf_ctx* ctx, const char* path, const uint64_t* offsets, const uint32_t* sizes,
+                               uint64_t n, const uint8_t* expected, uint8_t* out) {
+  if (!ctx || !path) return fail(LBF_ERR_INVALID, "null context/path");
+  return lbf_files_ranges(ctx, &path, 1, nullptr, offsets, sizes, n, expected, out);
 }
 
 extern "C" int lbf_sha1_one(lbf_ctx* ctx, const uint8_t* data, uint32_t size, uint8_t out[20]) {

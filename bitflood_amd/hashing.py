@@ -169,6 +169,37 @@ class ChunkHasher:
                                             offs.size, exp.ctypes.data, ver.ctypes.data))
         return ver.astype(bool)
 
+    def _files_call(self, paths, file_of, offsets, sizes, expected):
+        enc = [os.fsencode(p) for p in paths]
+        arr = (ctypes.c_char_p * len(enc))(*enc)
+        offs = np.ascontiguousarray(offsets, dtype=np.uint64)
+        szs = np.ascontiguousarray(sizes, dtype=np.uint32)
+        fo = np.ascontiguousarray(file_of, dtype=np.uint32)
+        if not (offs.shape == szs.shape == fo.shape):
+            raise ValueError("file_of, offsets and sizes differ in length")
+        if expected is None:
+            out = np.zeros((offs.size, DIGEST), dtype=np.uint8)
+            exp_ptr = None
+        else:
+            exp = np.ascontiguousarray(expected, dtype=np.uint8).reshape(-1, DIGEST)
+            if exp.shape[0] != offs.size:
+                raise ValueError("expected differs in length")
+            out = np.zeros(offs.size, dtype=np.uint8)
+            exp_ptr = exp.ctypes.data
+        if offs.size:
+            check(self._lib.lbf_files_ranges(self._h, arr, len(enc), fo.ctypes.data, offs.ctypes.data,
+                                             szs.ctypes.data, offs.size, exp_ptr, out.ctypes.data))
+        return out
+
+    def hash_files(self, paths, file_of, offsets, sizes) -> np.ndarray:
+        """Digests of byte ranges of several files in one pipelined batch
+        (lbf_files_ranges): chunk i = [offsets[i], +sizes[i]) of paths[file_of[i]]."""
+        return self._files_call(paths, file_of, offsets, sizes, None)
+
+    def verify_files(self, paths, file_of, offsets, sizes, expected) -> np.ndarray:
+        """Resume verify over several files in one batch (Flood.cpp:239-287)."""
+        return self._files_call(paths, file_of, offsets, sizes, expected).astype(bool)
+
     def sha1(self, data) -> bytes:
         buf = _as_u8(data)
         out = (ctypes.c_uint8 * DIGEST)()

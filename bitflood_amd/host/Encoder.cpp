@@ -11,6 +11,7 @@
 
 #include <mutex>
 #include <string>
+#include <vector>
 
 #include "lbf_hash.h"
 
@@ -96,6 +97,11 @@ Error::ErrorCode Base64EncodeBatch(const U8* i_base, U64 i_len, const U64* i_off
   return Error::NO_ERROR_LBF;
 }
 
+// Encoder.cpp:17-102.  The reference hashes its files one after another; here
+// every existing file's chunks go to the GPU in ONE pipelined batch
+// (lbf_files_ranges), because each chunk's serial SHA-1 chain costs the same
+// whatever the batch: per-file calls would pay ≈3 ms per file at 256 KiB
+// chunks.  Results and error behaviour are the reference's.
 Error::ErrorCode EncodeFile(const ToEncode& i_toencode, FloodFile& o_floodfile) {
   Error::ErrorCode ret = Error::NO_ERROR_LBF;
   FloodFile toReturn;
@@ -106,6 +112,10 @@ Error::ErrorCode EncodeFile(const ToEncode& i_toencode, FloodFile& o_floodfile) 
     lbf_ctx* ctx = Context();
     if (!ctx) return Error::UNKNOWN_ERROR_LBF;
     const U64 cs = i_toencode.m_chunksize;
+    std::vector<const char*> paths;  // files that exist, in the given order
+    std::vector<U64> size_of, first_of;
+    V_U64 offs;
+    V_U32 sizes, file_of;
     for (const std::string& path : i_toencode.m_files) {  // in the given order, like :40
       struct stat st;
       if (stat(path.c_str(), &st) != 0 || S_ISDIR(st.st_mode)) {
@@ -115,30 +125,37 @@ Error::ErrorCode EncodeFile(const ToEncode& i_toencode, FloodFile& o_floodfile) 
       }
       const U64 size = (U64)st.st_size;
       const U64 n = (size + cs - 1) / cs;  // the fread loop's chunk count (:54-72)
-      V_U64 offs(n);
-      V_U32 sizes(n);
+      const U32 f = (U32)paths.size();
+      paths.push_back(path.c_str());
+      size_of.push_back(size);
+      first_of.push_back(offs.size());
       for (U64 i = 0; i < n; ++i) {
-        offs[i] = i * cs;
-        sizes[i] = (U32)std::min<U64>(cs, size - i * cs);
+        offs.push_back(i * cs);
+        sizes.push_back((U32)std::min<U64>(cs, size - i * cs));
+        file_of.push_back(f);
       }
-      V_U8 digests(n * 20);
-      if (n && lbf_file_ranges(ctx, path.c_str(), offs.data(), sizes.data(), n, nullptr, digests.data()) != LBF_OK) {
-        fail("EncodeFile(" + path + ")");
-        ret = Error::UNKNOWN_ERROR_LBF;
-        continue;
+    }
+    V_U8 digests(offs.size() * 20);
+    if (!offs.empty() && lbf_files_ranges(ctx, paths.data(), (U32)paths.size(), file_of.data(), offs.data(),
+                                          sizes.data(), offs.size(), nullptr, digests.data()) != LBF_OK) {
+      fail("EncodeFile");
+      ret = Error::UNKNOWN_ERROR_LBF;
+    } else {
+      for (size_t f = 0; f < paths.size(); ++f) {
+        const U64 first = first_of[f], n = (f + 1 < paths.size() ? first_of[f + 1] : offs.size()) - first;
+        FloodFile::FileSPtr file(new FloodFile::File());
+        file->m_name = paths[f];
+        file->m_size = size_of[f];  // 64-bit; the reference's U32 wraps at 4 GiB (:76)
+        file->m_chunks.resize(n);
+        for (U64 i = 0; i < n; ++i) {
+          FloodFile::Chunk& c = file->m_chunks[i];
+          c.m_index = (U32)i;
+          c.m_size = sizes[first + i];
+          c.m_weight = 0;
+          c.m_hash = b64(&digests[20 * (first + i)]);
+        }
+        toReturn.m_files[paths[f]] = file;
       }
-      FloodFile::FileSPtr file(new FloodFile::File());
-      file->m_name = path;
-      file->m_size = size;  // 64-bit; the reference's U32 wraps at 4 GiB (:76)
-      file->m_chunks.resize(n);
-      for (U64 i = 0; i < n; ++i) {
-        FloodFile::Chunk& c = file->m_chunks[i];
-        c.m_index = (U32)i;
-        c.m_size = sizes[i];
-        c.m_weight = 0;
-        c.m_hash = b64(&digests[20 * i]);
-      }
-      toReturn.m_files[path] = file;
     }
     for (const ToEncode::Tracker& t : i_toencode.m_trackers) {  // :83-93
       FloodFile::TrackerInfo ti;

@@ -66,8 +66,9 @@ Error::ErrorCode Flood::Initialize(FloodFileSPtr& i_floodfile) {
 }
 
 // Flood.cpp:220-299.  Per file: lay the chunks out back to back in index
-// order, then hash every chunk that exists on disk in ONE batched verify (the
-// reference does fseek + malloc + fread + Base64Encode + strcmp per chunk).
+// order; then hash every chunk of every file that exists on disk in ONE
+// batched verify (lbf_files_ranges).  The reference does fseek + malloc +
+// fread + Base64Encode + strcmp per chunk, file after file.
 Error::ErrorCode Flood::SetupFilesAndChunks() {
   m_totalbytes = 0;
   m_runtimefiles.clear();
@@ -76,6 +77,13 @@ Error::ErrorCode Flood::SetupFilesAndChunks() {
   lbf_ctx* ctx = Ctx();
   if (!ctx) return Error::UNKNOWN_ERROR_LBF;
   Error::ErrorCode ret = Error::NO_ERROR_LBF;
+  std::vector<RuntimeFile> rtfs;
+  std::vector<std::string> paths;
+  std::vector<U64> first_of;
+  V_U64 offs;
+  V_U32 sizes, file_of;
+  V_U8 expected;
+  std::vector<U8> decodable;
   for (const auto& kv : m_floodfile->m_files) {
     const FloodFile::FileSPtr& file = kv.second;
     m_totalbytes += file->m_size;
@@ -85,10 +93,7 @@ Error::ErrorCode Flood::SetupFilesAndChunks() {
     rtf.m_chunkmap.assign(n, '0');
     rtf.m_file = file;
     // offsets follow chunk vector order (sorted by index in FromXML)
-    V_U64 offs(n);
-    V_U32 sizes(n);
-    V_U8 expected(n * 20, 0);
-    std::vector<U8> decodable(n, 0);
+    const U64 first = offs.size();
     U64 next = 0;
     bool indices_ok = true;
     std::vector<bool> seen(n, false);
@@ -100,24 +105,39 @@ Error::ErrorCode Flood::SetupFilesAndChunks() {
       }
       seen[c.m_index] = true;
       rtf.m_chunkoffsets[c.m_index] = next;
-      offs[k] = next;
-      sizes[k] = c.m_size;
-      decodable[k] = decode_hash(c.m_hash, &expected[20 * k]) ? 1 : 0;
+      offs.push_back(next);
+      sizes.push_back(c.m_size);
+      file_of.push_back((U32)paths.size());
+      expected.resize(expected.size() + 20, 0);
+      decodable.push_back(decode_hash(c.m_hash, &expected[expected.size() - 20]) ? 1 : 0);
       next += c.m_size;
     }
     if (!indices_ok) {  // the reference asserts (Flood.cpp:253-254)
+      offs.resize(first);
+      sizes.resize(first);
+      file_of.resize(first);
+      expected.resize(20 * first);
+      decodable.resize(first);
       ret = Error::UNKNOWN_ERROR_LBF;
       continue;
     }
-    V_U8 verdicts(n, 0);
-    if (n && lbf_file_ranges(ctx, PathOf(file->m_name).c_str(), offs.data(), sizes.data(), n, expected.data(),
-                             verdicts.data()) != LBF_OK) {
-      ret = Error::UNKNOWN_ERROR_LBF;
-      continue;
-    }
-    for (U64 k = 0; k < n; ++k) {
+    paths.push_back(PathOf(file->m_name));
+    first_of.push_back(first);
+    rtfs.push_back(rtf);
+  }
+  V_U8 verdicts(offs.size(), 0);
+  std::vector<const char*> cpaths;
+  for (const std::string& p : paths) cpaths.push_back(p.c_str());
+  if (!offs.empty() && lbf_files_ranges(ctx, cpaths.data(), (U32)cpaths.size(), file_of.data(), offs.data(),
+                                        sizes.data(), offs.size(), expected.data(), verdicts.data()) != LBF_OK)
+    return Error::UNKNOWN_ERROR_LBF;
+  for (size_t f = 0; f < rtfs.size(); ++f) {
+    RuntimeFile& rtf = rtfs[f];
+    const FloodFile::FileSPtr& file = rtf.m_file;
+    const U64 first = first_of[f];
+    for (U64 k = 0; k < file->m_chunks.size(); ++k) {
       const U32 idx = file->m_chunks[k].m_index;
-      if (verdicts[k] && decodable[k]) rtf.m_chunkmap[idx] = '1';
+      if (verdicts[first + k] && decodable[first + k]) rtf.m_chunkmap[idx] = '1';
       if (rtf.m_chunkmap[idx] == '0') m_chunkstodownload.insert(P_ChunkKey(file->m_name, idx));
     }
     m_runtimefiles[file->m_name] = rtf;

@@ -162,6 +162,38 @@ int main(int argc, char** argv) {
         CHECK(fe->m_chunks[i].m_index == i && fe->m_chunks[i].m_size == z[i] && fe->m_chunks[i].m_hash == want[i]);
       }
     }
+    // the same three files through the resume verify, batched over files
+    // (Flood.cpp:220-299): intact -> all '1'; then c.bin loses its tail,
+    // a.bin's second chunk gets a flipped byte, b.bin stays empty
+    {
+      FloodFileSPtr mff(new FloodFile(mf));
+      Flood mv;
+      CHECK(mv.Initialize(mff) == Error::NO_ERROR_LBF);
+      CHECK(mv.m_runtimefiles[files[0].first].m_chunkmap == "111");
+      CHECK(mv.m_runtimefiles[files[1].first].m_chunkmap == "11");
+      CHECK(mv.m_runtimefiles[files[2].first].m_chunkmap.empty());
+      CHECK(mv.m_chunkstodownload.empty());
+      FILE* g = std::fopen(files[0].first.c_str(), "wb");
+      std::fwrite(bytes[0].data(), 1, 65536 + 10, g);
+      std::fclose(g);
+      std::vector<U8> a = bytes[1];
+      a[65536 + 3] ^= 0x20;
+      g = std::fopen(files[1].first.c_str(), "wb");
+      std::fwrite(a.data(), 1, a.size(), g);
+      std::fclose(g);
+      Flood mv2;
+      CHECK(mv2.Initialize(mff) == Error::NO_ERROR_LBF);
+      CHECK(mv2.m_runtimefiles[files[0].first].m_chunkmap == "100");
+      CHECK(mv2.m_runtimefiles[files[1].first].m_chunkmap == "10");
+      CHECK(mv2.m_chunkstodownload.size() == 3);
+      // restore c.bin and a.bin for what follows
+      g = std::fopen(files[0].first.c_str(), "wb");
+      std::fwrite(bytes[0].data(), 1, bytes[0].size(), g);
+      std::fclose(g);
+      g = std::fopen(files[1].first.c_str(), "wb");
+      std::fwrite(bytes[1].data(), 1, bytes[1].size(), g);
+      std::fclose(g);
+    }
     // a missing file: the call fails and the output is left as it was (:45-47, :96-99)
     me.m_files.push_back(dir + "/missing.bin");
     FloodFile untouched;

@@ -110,6 +110,17 @@ int lbf_verify_batch(lbf_ctx* ctx, const uint8_t* base, uint64_t base_len,
  *   reference leaves such chunks '0'. */
 int lbf_file_ranges(lbf_ctx* ctx, const char* path, const uint64_t* offsets, const uint32_t* sizes,
                     uint64_t n, const uint8_t* expected, uint8_t* out);
+/* The same over several files in ONE pipelined batch: chunk i is bytes
+ * [offsets[i], offsets[i] + sizes[i]) of paths[file_of[i]] (file_of may be
+ * NULL when n_files == 1).  This is EncodeFile's loop over m_files
+ * (Encoder.cpp:40-79) and _SetupFilesAndChunks' loop over the flood's files
+ * (Flood.cpp:239-287) as one call: every chunk's serial SHA-1 chain costs the
+ * same whatever the batch, so per-file calls pay it once per file.  Per-chunk
+ * semantics as lbf_file_ranges; a file that cannot be opened fails hash mode
+ * with LBF_ERR_IO and gives verdict 0 to all its chunks in verify mode. */
+int lbf_files_ranges(lbf_ctx* ctx, const char* const* paths, uint32_t n_files, const uint32_t* file_of,
+                     const uint64_t* offsets, const uint32_t* sizes, uint64_t n, const uint8_t* expected,
+                     uint8_t* out);
 
 /* ---- single buffer (Encoder::Base64Encode's hash, host memory) ---------- */
 int lbf_sha1_one(lbf_ctx* ctx, const uint8_t* data, uint32_t size, uint8_t out_digest[20]);

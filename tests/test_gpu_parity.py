@@ -350,3 +350,56 @@ def test_unsorted_overlapping_duplicate_table(hasher, oracle):
     flips = [0, 7, 21, 22, 300, len(offs) - 1]
     exp[flips, 19] ^= 1
     assert np.flatnonzero(~hasher.verify_chunks(buf, offs, sizes, exp)).tolist() == flips
+
+
+def test_hash_and_verify_many_files_one_batch(hasher, oracle, tmp_path):
+    """lbf_files_ranges: EncodeFile's and _SetupFilesAndChunks' loops over a
+    flood's files (Encoder.cpp:40-79, Flood.cpp:239-287) as ONE batch.  40 files
+    of assorted sizes (empty, sub-chunk, ragged tails), descriptors interleaved
+    across files; verify with a truncated file, a missing file (all '0', its
+    empty chunk too) and a flipped byte."""
+    rng = np.random.default_rng(40)
+    cs = 65536 + 13
+    paths, datas = [], []
+    for f in range(40):
+        size = int(rng.choice([0, 1, 100, cs, 3 * cs + 7, int(rng.integers(0, 2 << 20))]))
+        d = oracle.synth(500 + f, 0, size)
+        p = tmp_path / f"f{f:02d}.bin"
+        p.write_bytes(d.tobytes())
+        paths.append(str(p))
+        datas.append(d)
+    file_of, offs, sizes = [], [], []
+    for f, d in enumerate(datas):
+        o, s = chunk_table(d.size, cs)
+        if d.size == 0:  # an empty file still contributes an empty chunk here
+            o, s = np.zeros(1, np.uint64), np.zeros(1, np.uint32)
+        file_of += [f] * o.size
+        offs += o.tolist()
+        sizes += s.tolist()
+    perm = rng.permutation(len(offs))  # interleave files and chunks
+    file_of = np.array(file_of, np.uint32)[perm]
+    offs = np.array(offs, np.uint64)[perm]
+    sizes = np.array(sizes, np.uint32)[perm]
+    want = np.stack([oracle.sha1(datas[f][o:o + s].tobytes()) if s else oracle.sha1(b"")
+                     for f, o, s in zip(file_of, offs.astype(np.int64), sizes.astype(np.int64))]).view(np.uint8)
+    want = want.reshape(-1, 20)
+    assert np.array_equal(hasher.hash_files(paths, file_of, offs, sizes), want)
+    assert hasher.verify_files(paths, file_of, offs, sizes, want).all()
+    # damage: file 3 truncated to half, file 7 missing, one byte of file 11 flipped
+    big = [f for f in range(40) if datas[f].size > 2 * cs][:3]
+    t, m, x = big
+    cut = datas[t].size // 2
+    open(paths[t], "wb").write(datas[t][:cut].tobytes())
+    import os as _os
+    _os.remove(paths[m])
+    bad = datas[x].copy()
+    bad[cs + 5] ^= 1
+    open(paths[x], "wb").write(bad.tobytes())
+    v = hasher.verify_files(paths, file_of, offs, sizes, want)
+    exp_v = np.ones(len(offs), bool)
+    exp_v[(file_of == t) & (offs.astype(np.int64) + sizes > cut) & (sizes > 0)] = False
+    exp_v[file_of == m] = False
+    exp_v[(file_of == x) & (offs == np.uint64(cs))] = False
+    assert np.array_equal(v, exp_v)
+    with pytest.raises(Exception):
+        hasher.hash_files(paths, file_of, offs, sizes)  # a missing file fails hash mode

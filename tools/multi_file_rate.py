@@ -1,0 +1,55 @@
+#!/usr/bin/env python3
+"""Many files, one batch vs one call per file (diagnostic, GPU box).
+
+Writes N files of S bytes (page-cache warm), then times their resume verify /
+hash at 256 KiB chunks two ways: one lbf_file_ranges call per file (what a
+per-file loop costs: each call pays at least one serial SHA-1 chain, ≈3 ms at
+256 KiB) and one lbf_files_ranges batch over all of them.  Checks that both give
+the same digests.  Usage: python tools/multi_file_rate.py [--files 512] [--mib 8]
+"""
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+import numpy as np
+import torch  # noqa: F401  (one HIP runtime, loaded first)
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bitflood_amd import ChunkHasher, chunk_table  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--files", type=int, default=512)
+ap.add_argument("--mib", type=float, default=8)
+a = ap.parse_args()
+CS = 262144
+size = int(a.mib * (1 << 20))
+rng = np.random.default_rng(9)
+with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as d:
+    paths = []
+    for f in range(a.files):
+        p = os.path.join(d, f"f{f:05d}.bin")
+        rng.integers(0, 256, size, dtype=np.uint8).tofile(p)
+        paths.append(p)
+    o, s = chunk_table(size, CS)
+    file_of = np.repeat(np.arange(a.files, dtype=np.uint32), o.size)
+    offs, sizes = np.tile(o, a.files), np.tile(s, a.files)
+    out = {"files": a.files, "bytes_per_file": size, "chunk_size": CS}
+    with ChunkHasher(device_mask=1) as h:
+        h.hash_files(paths, file_of, offs, sizes)  # warm: staging sized
+        best_loop = best_batch = 1e9
+        for _ in range(3):
+            t = time.perf_counter()
+            per = [h.hash_file(p, o, s) for p in paths]
+            best_loop = min(best_loop, time.perf_counter() - t)
+            t = time.perf_counter()
+            batch = h.hash_files(paths, file_of, offs, sizes)
+            best_batch = min(best_batch, time.perf_counter() - t)
+        assert np.array_equal(np.concatenate(per), batch)
+    total = a.files * size / 2**30
+    out["per_file_calls_gibs"] = round(total / best_loop, 2)
+    out["one_batch_gibs"] = round(total / best_batch, 2)
+    out["speedup"] = round(best_loop / best_batch, 2)
+    print(json.dumps(out))
