@@ -5,7 +5,8 @@
 // staging slots, slot size, an injected one-shot group fault) and a batch
 // (ragged, unaligned, empty and oversize chunks), then checks
 //   lbf_sha1_batch / lbf_verify_batch (host memory) and
-//   lbf_file_ranges (hash and verify, including a truncated file)
+//   lbf_file_ranges (hash and verify, including a truncated file) and
+//   lbf_files_ranges (verify over 2-4 truncated or missing files)
 // against the oracle (oracle/sha1_oracle.c, compiled in as the checker).
 //   asan_capi <scratch-dir> [seconds] [seed]
 #include <fcntl.h>
@@ -140,6 +141,40 @@ int main(int argc, char** argv) {
       } else {
         CHECK(rc == LBF_ERR_IO, "file hash of a truncated file rc %d: %s", rc, lbf_last_error());
       }
+      // several files at once (lbf_files_ranges): the buffer's bytes spread over
+      // 2-4 files that each hold a copy truncated at its own length, one maybe
+      // missing; every chunk names a random file
+      const uint32_t nf = (uint32_t)uni(2, 4);
+      std::vector<std::string> fpaths(nf);
+      std::vector<uint64_t> fkeep(nf);
+      std::vector<bool> fmissing(nf, false);
+      for (uint32_t f = 0; f < nf; ++f) {
+        fpaths[f] = dir + "/asan_capi_f" + std::to_string(f) + ".bin";
+        fmissing[f] = uni(0, 5) == 0;
+        fkeep[f] = uni(0, 2) ? buf_len : uni(0, buf_len);
+        unlink(fpaths[f].c_str());
+        if (fmissing[f]) continue;
+        const int g = open(fpaths[f].c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
+        CHECK(g >= 0 && write(g, buf.data(), fkeep[f]) == (ssize_t)fkeep[f], "write %s", fpaths[f].c_str());
+        close(g);
+      }
+      std::vector<const char*> cp(nf);
+      for (uint32_t f = 0; f < nf; ++f) cp[f] = fpaths[f].c_str();
+      std::vector<uint32_t> file_of(n);
+      for (uint64_t i = 0; i < n; ++i) file_of[i] = (uint32_t)uni(0, nf - 1);
+      std::vector<uint8_t> mver(n, 7);
+      rc = lbf_files_ranges(ctx, cp.data(), nf, file_of.data(), off.data(), size.data(), n, want.data(), mver.data());
+      if (rc == LBF_ERR_HIP && strstr(lbf_last_error(), "injected fault")) {
+        ++faults;
+        rc = lbf_files_ranges(ctx, cp.data(), nf, file_of.data(), off.data(), size.data(), n, want.data(), mver.data());
+      }
+      CHECK(rc == LBF_OK, "files verify rc %d: %s", rc, lbf_last_error());
+      for (uint64_t i = 0; i < n && rc == LBF_OK; ++i) {
+        const uint32_t f = file_of[i];
+        const bool present = !fmissing[f] && (size[i] == 0 || off[i] + size[i] <= fkeep[f]);
+        CHECK(mver[i] == (present ? 1 : 0), "files verdict %lu (file %u)", (unsigned long)i, f);
+      }
+      for (uint32_t f = 0; f < nf; ++f) unlink(fpaths[f].c_str());
     }
     lbf_ctx_destroy(ctx);
   }
