@@ -287,23 +287,36 @@ int page_node(const void* p) {
 }
 
 // ---- workers and slots -----------------------------------------------------
-// A slot's device and pinned buffers are laid out [header | data]: the
-// header holds one group's descriptors (offsets u64[cnt], sizes u32[cnt],
-// expected 20 B x cnt), padded to kHdrAlign, and the chunk bytes follow.  One
-// H2D moves a whole group, one D2H returns its digests or verdicts.
+// Staging is split in two rings.  A HOST slot is pinned memory laid out
+// [header | data]: the header holds one group's descriptors (offsets u64[cnt],
+// sizes u32[cnt], expected 20 B x cnt), padded to kHdrAlign, and the chunk
+// bytes follow.  A DEVICE slot is the same layout in HBM plus its stream and
+// the group's results.  One H2D moves a whole group from a host slot to a
+// device slot, one kernel hashes it there, one D2H returns its digests or
+// verdicts.  A host slot is free again as soon as its H2D is done; a device
+// slot only once its kernel is -- and that kernel lasts one chunk's serial
+// SHA-1 chain (≈3.1 ms per 256 KiB of chunk, whatever the group size).  So the
+// device ring is sized per job to hold PCIe-rate x chain-time bytes in HBM
+// (288 GB per GPU: it is the cheap place for bytes in flight), while the
+// pinned ring stays at LBF_SLOTS.
 constexpr uint64_t kHdrAlign = 256;
 constexpr uint64_t kDescBytes = 8 + 4 + 20;
 
 uint64_t header_bytes(uint64_t cnt) { return (cnt * kDescBytes + kHdrAlign - 1) / kHdrAlign * kHdrAlign; }
 
-struct Slot {
+struct HostSlot {
+  uint8_t* h_buf = nullptr;      // pinned, hdr_cap + slot_bytes
+  hipEvent_t copied = nullptr;   // recorded after the H2D that last read h_buf
+  bool in_flight = false;
+};
+
+struct DevSlot {
   hipStream_t stream = nullptr;
   uint8_t* d_buf = nullptr;  // header | data (hdr_cap + slot_bytes)
-  uint8_t* h_buf = nullptr;  // pinned mirror
   uint8_t* d_out = nullptr;  // desc_cap * 20: digests, or verdicts
   uint8_t* h_out = nullptr;  // pinned
   std::vector<uint8_t> ok;   // 1 = chunk bytes fully available
-  // pending group to finalize after the stream drains
+  // pending group (positions [g_begin, g_end)) to finalize after the stream drains
   bool pending = false;
   uint64_t g_begin = 0, g_end = 0;
 };
@@ -313,9 +326,11 @@ struct Worker {
   int index = 0;            // position in the context
   int numa_node = -1;       // the device's NUMA node (-1: unknown / placement off)
   std::vector<int> cpus;    // CPUs its host threads bind to (empty: unbound)
-  std::vector<Slot> slot;   // LBF_SLOTS of them (default 3), used round-robin
+  std::vector<HostSlot> host;  // LBF_SLOTS of them (default 3), used round-robin
+  std::vector<DevSlot> dev;    // at least as many; grown per job for long chains, trimmed after it
   uint64_t slot_bytes = 0;  // current data capacity per slot (grown on demand)
   uint64_t slot_max = 0;    // LBF_SLOT_MB: the largest a slot may grow
+  uint64_t dev_budget = 0;  // LBF_DEVICE_STAGING_MB: HBM for device slots
   uint64_t desc_cap = 0;    // descriptors per group
   uint64_t hdr_cap = 0;     // header_bytes(desc_cap)
   long fault_group = -1;    // LBF_TEST_FAULT_GROUP (tests only, one shot)
@@ -340,39 +355,91 @@ hipError_t host_alloc(const Worker& w, void** p, uint64_t bytes) {
   return hipHostMalloc(p, bytes, hipHostMallocDefault);
 }
 
+int dev_slot_init(Worker& w, DevSlot& d) {
+  LBF_HIP_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+  LBF_HIP_TRY(hipMalloc((void**)&d.d_out, w.desc_cap * 20));
+  LBF_HIP_TRY(host_alloc(w, (void**)&d.h_out, w.desc_cap * 20));
+  if (w.slot_bytes) LBF_HIP_TRY(hipMalloc((void**)&d.d_buf, w.hdr_cap + w.slot_bytes));
+  d.ok.assign(w.desc_cap, 0);
+  return LBF_OK;
+}
+
+void dev_slot_free(DevSlot& d) {
+  // errors here have nowhere to go: the slot is being released
+  if (d.stream) (void)hipStreamSynchronize(d.stream);
+  if (d.d_buf) (void)hipFree(d.d_buf);
+  if (d.d_out) (void)hipFree(d.d_out);
+  if (d.h_out) (void)hipHostFree(d.h_out);
+  if (d.stream) (void)hipStreamDestroy(d.stream);
+  d = DevSlot{};
+}
+
 // Staging memory is sized to the work, not reserved up front: pinning 2 x 512
 // MiB costs ≈200 ms at context creation and ≈110 ms at destruction
 // (tools/startup_probe.py), which a one-chunk Base64Encode or a small file
-// should not pay.  A slot grows, never shrinks, in 8 MiB steps up to slot_max.
+// should not pay.  Slots grow, never shrink, in 8 MiB steps up to slot_max.
 constexpr uint64_t kSlotStep = 8ull << 20;
 
 int ensure_slot_bytes(Worker& w, uint64_t need) {
   need = std::min(w.slot_max, (std::max(need, kSlotStep) + kSlotStep - 1) / kSlotStep * kSlotStep);
   if (need <= w.slot_bytes) return LBF_OK;
-  for (Slot& s : w.slot) {
-    LBF_HIP_TRY(hipStreamSynchronize(s.stream));
-    if (s.d_buf) (void)hipFree(s.d_buf);
-    if (s.h_buf) (void)hipHostFree(s.h_buf);
-    s.d_buf = nullptr;
-    s.h_buf = nullptr;
+  for (DevSlot& d : w.dev) {
+    LBF_HIP_TRY(hipStreamSynchronize(d.stream));
+    if (d.d_buf) (void)hipFree(d.d_buf);
+    d.d_buf = nullptr;
+  }
+  for (HostSlot& h : w.host) {
+    if (h.h_buf) (void)hipHostFree(h.h_buf);
+    h.h_buf = nullptr;
+    h.in_flight = false;
   }
   w.slot_bytes = 0;
-  for (Slot& s : w.slot) {
-    LBF_HIP_TRY(hipMalloc((void**)&s.d_buf, w.hdr_cap + need));
-    LBF_HIP_TRY(host_alloc(w, (void**)&s.h_buf, w.hdr_cap + need));
-  }
+  for (DevSlot& d : w.dev) LBF_HIP_TRY(hipMalloc((void**)&d.d_buf, w.hdr_cap + need));
+  for (HostSlot& h : w.host) LBF_HIP_TRY(host_alloc(w, (void**)&h.h_buf, w.hdr_cap + need));
   w.slot_bytes = need;
   return LBF_OK;
+}
+
+// Device slots for a job whose longest staged chunk is `largest` bytes: enough
+// to keep ≈50 GB/s of H2D going for one chain's duration (≈1 µs per 64-byte
+// block, conservatively), at least one per host slot, at most the HBM budget.
+int ensure_dev_slots(Worker& w, uint64_t largest, uint64_t groups) {
+  const double chain_us = ((double)largest / 64.0 + 2.0) * 1.0;
+  const uint64_t in_flight = (uint64_t)(50e3 * chain_us);  // bytes at 50 GB/s
+  const uint64_t per = w.hdr_cap + w.slot_bytes;
+  uint64_t want = (in_flight + w.slot_bytes - 1) / std::max<uint64_t>(1, w.slot_bytes) + 1;
+  want = std::min<uint64_t>(want, groups);
+  want = std::min<uint64_t>(want, std::max<uint64_t>(1, w.dev_budget / per));
+  want = std::min<uint64_t>(32, std::max<uint64_t>(want, w.host.size()));
+  while (w.dev.size() < want) {
+    w.dev.emplace_back();
+    if (int rc = dev_slot_init(w, w.dev.back())) {
+      std::string msg = lbf_last_error();
+      dev_slot_free(w.dev.back());
+      w.dev.pop_back();
+      if (w.dev.size() >= w.host.size()) break;  // fewer slots in flight: slower, not wrong
+      return fail(rc, msg);
+    }
+  }
+  return LBF_OK;
+}
+
+// After a job, give back the device slots beyond one per host slot.
+void trim_dev_slots(Worker& w) {
+  while (w.dev.size() > w.host.size()) {
+    dev_slot_free(w.dev.back());
+    w.dev.pop_back();
+  }
 }
 
 int worker_init(Worker& w, int device, int index) {
   w.device = device;
   w.index = index;
   w.slot_max = std::max<uint64_t>(env_u64("LBF_SLOT_MB", 512) << 20, 1ull << 20);
-  // Three slots keep the PCIe link busy: with two, staging group g+2 waits for
-  // group g's H2D *and* its kernel (one chunk's serial chain, ≈3.2 ms at 256 KiB
-  // whatever the group size), so the link idles once per pair of groups.
-  w.slot.resize(std::min<uint64_t>(8, std::max<uint64_t>(2, env_u64("LBF_SLOTS", 3))));
+  w.dev_budget = std::max<uint64_t>(env_u64("LBF_DEVICE_STAGING_MB", 16384) << 20, 1ull << 20);
+  // Three pinned slots keep the PCIe link busy: with two, staging group g+2
+  // waits for group g's H2D, so the link idles while the host copies.
+  w.host.resize(std::min<uint64_t>(8, std::max<uint64_t>(2, env_u64("LBF_SLOTS", 3))));
   w.slot_bytes = 0;
   w.desc_cap = 1u << 16;
   w.hdr_cap = header_bytes(w.desc_cap);
@@ -384,26 +451,22 @@ int worker_init(Worker& w, int device, int index) {
     w.numa_node = device_numa_node(device);
     w.cpus = node_cpus_allowed(w.numa_node);
   }
-  for (Slot& s : w.slot) {
-    LBF_HIP_TRY(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
-    LBF_HIP_TRY(hipMalloc((void**)&s.d_out, w.desc_cap * 20));
-    LBF_HIP_TRY(host_alloc(w, (void**)&s.h_out, w.desc_cap * 20));
-    s.ok.assign(w.desc_cap, 0);
-  }
+  for (HostSlot& h : w.host) LBF_HIP_TRY(hipEventCreateWithFlags(&h.copied, hipEventDisableTiming));
+  w.dev.resize(w.host.size());
+  for (DevSlot& d : w.dev)
+    if (int rc = dev_slot_init(w, d)) return rc;
   return LBF_OK;
 }
 
 void worker_free(Worker& w) {
   if (hipSetDevice(w.device) != hipSuccess) return;
-  for (Slot& s : w.slot) {
-    // teardown: errors here have nowhere to go, the context is being destroyed
-    if (s.stream) (void)hipStreamSynchronize(s.stream);
-    if (s.d_buf) (void)hipFree(s.d_buf);
-    if (s.d_out) (void)hipFree(s.d_out);
-    if (s.h_buf) (void)hipHostFree(s.h_buf);
-    if (s.h_out) (void)hipHostFree(s.h_out);
-    if (s.stream) (void)hipStreamDestroy(s.stream);
-    s = Slot{};
+  // teardown: errors here have nowhere to go, the context is being destroyed
+  for (DevSlot& d : w.dev) dev_slot_free(d);
+  w.dev.clear();
+  for (HostSlot& h : w.host) {
+    if (h.h_buf) (void)hipHostFree(h.h_buf);
+    if (h.copied) (void)hipEventDestroy(h.copied);
+    h = HostSlot{};
   }
 }
 
@@ -519,7 +582,7 @@ struct Order {
 // Copy finished results of a slot's group (positions [g_begin, g_end)) to the
 // caller's arrays.  Chunks that were not fully readable: verdict 0 (verify) or
 // an LBF_ERR_IO (hash).
-int finalize(const Job& job, const Order& order, Slot& s) {
+int finalize(const Job& job, const Order& order, DevSlot& s) {
   if (!s.pending) return LBF_OK;
   s.pending = false;
   const uint64_t cnt = s.g_end - s.g_begin;
@@ -538,9 +601,11 @@ int finalize(const Job& job, const Order& order, Slot& s) {
   return LBF_OK;
 }
 
-// One chunk that does not fit a slot: a dedicated device buffer, synchronous.
+// One chunk that does not fit a slot: a dedicated device buffer, synchronous
+// (device slot 0's stream and host slot 0's header, both idle by then).
 int run_oversize(Worker& w, const Job& job, uint64_t i) {
-  Slot& s = w.slot[0];
+  DevSlot& s = w.dev[0];
+  HostSlot& h = w.host[0];
   LBF_HIP_TRY(hipStreamSynchronize(s.stream));
   const uint32_t sz = job.sizes[i];
   std::vector<uint8_t> host(sz ? sz : 1);
@@ -560,11 +625,11 @@ int run_oversize(Worker& w, const Job& job, uint64_t i) {
   do {
     // header of a one-chunk group: offset 0, size sz, expected digest
     const uint64_t off0 = 0;
-    memcpy(s.h_buf, &off0, 8);
-    memcpy(s.h_buf + 8, &sz, 4);
-    if (job.expected) memcpy(s.h_buf + 12, job.expected + 20 * i, 20);
+    memcpy(h.h_buf, &off0, 8);
+    memcpy(h.h_buf + 8, &sz, 4);
+    if (job.expected) memcpy(h.h_buf + 12, job.expected + 20 * i, 20);
     if (hipMemcpy(d, host.data(), sz, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(s.d_buf, s.h_buf, kDescBytes, hipMemcpyHostToDevice) != hipSuccess) {
+        hipMemcpy(s.d_buf, h.h_buf, kDescBytes, hipMemcpyHostToDevice) != hipSuccess) {
       rc = fail(LBF_ERR_HIP, "oversize chunk H2D failed");
       break;
     }
@@ -585,14 +650,6 @@ int run_oversize(Worker& w, const Job& job, uint64_t i) {
   return rc;
 }
 
-// Process descriptors [begin, end) on one worker.  Groups of consecutive
-// descriptors whose covering byte range fits a slot are staged into pinned
-// memory (memcpy or pread), then one H2D + kernel + one D2H run on the slot's
-// stream while the host stages the next group into the next slot.
-//
-// Every exit, error or not, passes the drain at the end: each slot's stream is
-// synchronized and its pending group cleared, so nothing is still in flight
-// and no stale group can be finalized into the next job's arrays.
 // Descriptors closer than this to the end of the current run join it: the gap
 // is copied along (cheaper than another copy); the 16-byte padding between
 // ReadVerifiedChunks' arena slots is the common case.
@@ -653,10 +710,13 @@ int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
       }
     }
     const uint64_t per = bytes <= kSplitMin ? bytes : std::max({kSplitMin, (bytes + 3) / 4, largest});
-    if (end > begin)
+    if (end > begin) {
       if (int rc = ensure_slot_bytes(w, std::min(per, w.slot_max) + 16)) return rc;  // nothing pending yet
+      const uint64_t groups = bytes / std::max<uint64_t>(1, w.slot_bytes) + 2;
+      if (int rc = ensure_dev_slots(w, largest, groups)) return rc;
+    }
   }
-  int cur = 0;
+  int cur = 0, hcur = 0;
   uint64_t i = begin;
   int rc = LBF_OK;
   long group = 0;
@@ -669,7 +729,7 @@ int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
   };
   while (i < end && rc == LBF_OK) {
     if ((uint64_t)job.sizes[order(i)] + 15 > w.slot_bytes) {
-      for (Slot& s : w.slot) {
+      for (DevSlot& s : w.dev) {
         if (!hip_ok(hipStreamSynchronize(s.stream), "hipStreamSynchronize")) break;
         if ((rc = finalize(job, order, s))) break;
       }
@@ -704,7 +764,7 @@ int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
       run_of.push_back((uint32_t)(runs.size() - 1));
       ++j;
     }
-    Slot& s = w.slot[cur];
+    DevSlot& s = w.dev[cur];
     if (!hip_ok(hipStreamSynchronize(s.stream), "hipStreamSynchronize")) break;
     if ((rc = finalize(job, order, s))) break;
     if (group++ == w.fault_group) {
@@ -712,12 +772,15 @@ int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
       rc = fail(LBF_ERR_HIP, "injected fault (LBF_TEST_FAULT_GROUP) at group " + std::to_string(group - 1));
       break;
     }
+    HostSlot& h = w.host[hcur];
+    if (h.in_flight && !hip_ok(hipEventSynchronize(h.copied), "hipEventSynchronize")) break;  // its last H2D is done
+    h.in_flight = false;
     const uint64_t cnt = j - i;
     const uint64_t hdr = header_bytes(cnt);
-    uint64_t* h_off = reinterpret_cast<uint64_t*>(s.h_buf);
-    uint32_t* h_size = reinterpret_cast<uint32_t*>(s.h_buf + 8 * cnt);
-    uint8_t* h_exp = s.h_buf + 12 * cnt;
-    read_runs(job.src, runs, s.h_buf + hdr, w.cpus);
+    uint64_t* h_off = reinterpret_cast<uint64_t*>(h.h_buf);
+    uint32_t* h_size = reinterpret_cast<uint32_t*>(h.h_buf + 8 * cnt);
+    uint8_t* h_exp = h.h_buf + 12 * cnt;
+    read_runs(job.src, runs, h.h_buf + hdr, w.cpus);
     for (uint64_t q = 0; q < cnt; ++q) {
       const uint64_t k = order(i + q), o = job.offsets[k], sz = job.sizes[k];
       const uint32_t r = run_of[q];
@@ -731,8 +794,10 @@ int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
       h_size[q] = s.ok[q] ? (uint32_t)sz : 0;
       if (job.expected) memcpy(h_exp + 20 * q, job.expected + 20 * k, 20);
     }
-    if (!hip_ok(hipMemcpyAsync(s.d_buf, s.h_buf, hdr + cursor, hipMemcpyHostToDevice, s.stream), "hipMemcpyAsync(H2D)"))
+    if (!hip_ok(hipMemcpyAsync(s.d_buf, h.h_buf, hdr + cursor, hipMemcpyHostToDevice, s.stream), "hipMemcpyAsync(H2D)") ||
+        !hip_ok(hipEventRecord(h.copied, s.stream), "hipEventRecord"))
       break;
+    h.in_flight = true;
     const uint64_t* d_off = reinterpret_cast<const uint64_t*>(s.d_buf);
     const uint32_t* d_size = reinterpret_cast<const uint32_t*>(s.d_buf + 8 * cnt);
     if (job.expected) rc = lbf_sha1_launch(s.d_buf + hdr, d_off, d_size, cnt, nullptr, s.d_buf + 12 * cnt, s.d_out, s.stream);
@@ -744,16 +809,20 @@ int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
     s.pending = true;
     s.g_begin = i;
     s.g_end = j;
-    cur = (cur + 1) % (int)w.slot.size();
+    cur = (cur + 1) % (int)w.dev.size();
+    hcur = (hcur + 1) % (int)w.host.size();
     i = j;
   }
-  // drain, on every path
-  for (Slot& s : w.slot) {
+  // drain, on every path (every H2D ran on a device slot's stream, so this also
+  // completes every host slot's copy)
+  for (DevSlot& s : w.dev) {
     const hipError_t e = hipStreamSynchronize(s.stream);
     if (e != hipSuccess && rc == LBF_OK) rc = hip_fail(e, "hipStreamSynchronize");
     if (rc == LBF_OK) rc = finalize(job, order, s);
     s.pending = false;
   }
+  for (HostSlot& h : w.host) h.in_flight = false;
+  trim_dev_slots(w);
   return rc;
 }
 
@@ -797,7 +866,7 @@ int run_device_job(lbf_ctx* ctx, const uint8_t* base, const uint64_t* offsets, c
   std::lock_guard<std::mutex> lock(ctx->mu);
   Worker& w = ctx->workers[0];
   LBF_HIP_TRY(hipSetDevice(w.device));
-  hipStream_t s = w.slot[0].stream;
+  hipStream_t s = w.dev[0].stream;
   for (uint64_t i = 0; i < n; i += 0xFFFFFFFFull) {
     const uint64_t cnt = std::min<uint64_t>(n - i, 0xFFFFFFFFull);
     int rc = lbf_sha1_launch(base, offsets + i, sizes + i, cnt, digests ? digests + 20 * i : nullptr,
@@ -846,7 +915,9 @@ extern "C" int lbf_ctx_worker_info(const lbf_ctx* ctx, int worker, int* device, 
   const Worker& w = ctx->workers[worker];
   if (device) *device = w.device;
   if (numa_node) *numa_node = w.numa_node;
-  if (staging_node) *staging_node = page_node(w.slot.empty() ? nullptr : (w.slot[0].h_buf ? w.slot[0].h_buf : w.slot[0].h_out));
+  if (staging_node)
+    *staging_node = page_node(!w.host.empty() && w.host[0].h_buf ? (const void*)w.host[0].h_buf
+                                                                 : (w.dev.empty() ? nullptr : (const void*)w.dev[0].h_out));
   if (bound_cpus) *bound_cpus = (int)w.cpus.size();
   return LBF_OK;
 }
