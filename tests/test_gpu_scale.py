@@ -107,3 +107,66 @@ def test_c4_all_shards(golden):
         H.set_kernel_variant(0)
         buf.free()
         dig.free()
+
+
+@pytest.mark.timeout(900)
+def test_c3_encode_file_cli_64_files(golden, tmp_path):
+    """C3 end to end through the C++ product path: lbf_encoder (test_encoder's
+    port) with the 64 x 1 GiB files of c3.json on disk (or /dev/shm), i.e.
+    Encoder::EncodeFile over 64 files (Encoder.cpp:17-102, batched over files),
+    then the flood file's 262,144 chunk strings are checked against the hashlib
+    goldens, and lbf_verify (Flood::SetupFilesAndChunks over the 64 files)
+    finds every chunk present."""
+    import base64
+    import json
+    import os
+    import re
+    import shutil
+    import subprocess
+    import tempfile
+    c3 = golden("c3.json")
+    fs = c3["file_size"]
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lib = os.path.join(root, "bitflood_amd", "lib")
+    shm_free = shutil.disk_usage("/dev/shm").free if os.path.isdir("/dev/shm") else 0
+    base = "/dev/shm" if shm_free > 80 * GIB else str(tmp_path)
+    d = tempfile.mkdtemp(prefix="lbf_c3_", dir=base)
+    try:
+        buf = DeviceBuffer(fs)
+        try:
+            names = []
+            for f in c3["files"]:
+                buf.fill_synthetic(f["seed"], start=0)
+                H.synchronize()
+                name = f"f{f['seed']:02d}.bin"
+                buf.download(fs).tofile(os.path.join(d, name))
+                names.append(name)
+        finally:
+            buf.free()
+        out = subprocess.run([os.path.join(lib, "lbf_encoder"), *names, "http://127.0.0.1:10101/", "c3.flood",
+                              "--time"], cwd=d, capture_output=True, text=True, timeout=600)
+        assert out.returncode == 0, out.stderr
+        t = json.loads(out.stdout.strip().splitlines()[-1])
+        print("C3 EncodeFile:", json.dumps(t), f"{t['bytes'] / GIB / t['encode_s']:.1f} GiB/s")
+        xml = open(os.path.join(d, "c3.flood")).read()
+        files = re.findall(r'<File name="([^"]+)" size="(\d+)">(.*?)</File>', xml, re.S)
+        assert [n for n, _, _ in files] == sorted(names)
+        allh = hashlib.sha1()
+        for (name, size, body), f in zip(files, c3["files"]):
+            assert int(size) == fs
+            hashes = re.findall(r'<Chunk hash="([^"]+)" index="(\d+)" size="(\d+)" weight="0"/>', body)
+            assert [int(i) for _, i, _ in hashes] == list(range(fs // c3["chunk_size"]))
+            raw = b"".join(base64.b64decode(h + "=") for h, _, _ in hashes)
+            allh.update(raw)
+            assert hashlib.sha1(raw).hexdigest() == f["sha1_of_concat_raw_digests_hex"], name
+            assert hashes[0][0] == f["first_b64"] and hashes[-1][0] == f["last_b64"]
+        assert allh.hexdigest() == c3["sha1_of_all_digests_in_file_order_hex"]
+        v = subprocess.run([os.path.join(lib, "lbf_verify"), "c3.flood", "--no-resolve"], cwd=d,
+                           capture_output=True, text=True, timeout=600)
+        assert v.returncode == 0, v.stderr
+        lines = dict(line.split(" ", 1) for line in v.stdout.strip().splitlines())
+        assert lines["to_download"] == "0"
+        for n in names:
+            assert lines[n].startswith("4096 4096 ")
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
