@@ -287,25 +287,27 @@ int page_node(const void* p) {
 }
 
 // ---- workers and slots -----------------------------------------------------
-// Staging is split in two rings.  A HOST slot is pinned memory laid out
-// [header | data]: the header holds one group's descriptors (offsets u64[cnt],
-// sizes u32[cnt], expected 20 B x cnt), padded to kHdrAlign, and the chunk
-// bytes follow.  A DEVICE slot is the same layout in HBM plus its stream and
-// the group's results.  One H2D moves a whole group from a host slot to a
-// device slot, one kernel hashes it there, one D2H returns its digests or
-// verdicts.  A host slot is free again as soon as its H2D is done; a device
-// slot only once its kernel is -- and that kernel lasts one chunk's serial
-// SHA-1 chain (≈3.1 ms per 256 KiB of chunk, whatever the group size).  So the
-// device ring is sized per job to hold PCIe-rate x chain-time bytes in HBM
-// (288 GB per GPU: it is the cheap place for bytes in flight), while the
-// pinned ring stays at LBF_SLOTS.
+// Staging is split in two rings.  A DEVICE slot in HBM holds one batch: the
+// descriptors (offsets u64[cnt], sizes u32[cnt], expected 20 B x cnt, padded
+// to kHdrAlign) and the chunk bytes, plus its stream and the batch's results;
+// one kernel hashes the batch there and one D2H returns digests or verdicts.
+// A HOST slot is a piece of pinned memory the batch's bytes pass through on
+// their way to the device slot: a batch larger than a host slot is copied as
+// several pieces (one H2D each) followed by its header, a batch that fits one
+// host slot travels as one [header | data] copy.  A host slot is free again
+// as soon as its H2D is done; a device slot only once its kernel is -- and
+// that kernel lasts one chunk's serial SHA-1 chain (≈3.1 ms per 256 KiB of
+// chunk, whatever the batch size).  So the device ring is sized per job to
+// hold PCIe-rate x chain-time bytes in HBM (288 GB per GPU: the cheap place
+// for bytes in flight), and the pinned ring stays small (LBF_SLOTS x
+// LBF_PIN_MB): pinning is what a one-shot encode pays up front.
 constexpr uint64_t kHdrAlign = 256;
 constexpr uint64_t kDescBytes = 8 + 4 + 20;
 
 uint64_t header_bytes(uint64_t cnt) { return (cnt * kDescBytes + kHdrAlign - 1) / kHdrAlign * kHdrAlign; }
 
 struct HostSlot {
-  uint8_t* h_buf = nullptr;      // pinned, hdr_cap + slot_bytes
+  uint8_t* h_buf = nullptr;      // pinned, pin_bytes
   hipEvent_t copied = nullptr;   // recorded after the H2D that last read h_buf
   bool in_flight = false;
 };
@@ -313,6 +315,7 @@ struct HostSlot {
 struct DevSlot {
   hipStream_t stream = nullptr;
   uint8_t* d_buf = nullptr;  // header | data (hdr_cap + slot_bytes)
+  uint8_t* h_hdr = nullptr;  // pinned header of a multi-piece batch (hdr_cap)
   uint8_t* d_out = nullptr;  // desc_cap * 20: digests, or verdicts
   uint8_t* h_out = nullptr;  // pinned
   std::vector<uint8_t> ok;   // 1 = chunk bytes fully available
@@ -328,8 +331,10 @@ struct Worker {
   std::vector<int> cpus;    // CPUs its host threads bind to (empty: unbound)
   std::vector<HostSlot> host;  // LBF_SLOTS of them (default 3), used round-robin
   std::vector<DevSlot> dev;    // at least as many; grown per job for long chains, trimmed after it
-  uint64_t slot_bytes = 0;  // current data capacity per slot (grown on demand)
-  uint64_t slot_max = 0;    // LBF_SLOT_MB: the largest a slot may grow
+  uint64_t slot_bytes = 0;  // current data capacity per device slot (grown on demand)
+  uint64_t slot_max = 0;    // LBF_SLOT_MB: the largest a device slot may grow
+  uint64_t pin_bytes = 0;   // current size of each pinned host slot (grown on demand)
+  uint64_t pin_max = 0;     // LBF_PIN_MB: the largest a host slot may grow
   uint64_t dev_budget = 0;  // LBF_DEVICE_STAGING_MB: HBM for device slots
   uint64_t desc_cap = 0;    // descriptors per group
   uint64_t hdr_cap = 0;     // header_bytes(desc_cap)
@@ -359,6 +364,7 @@ int dev_slot_init(Worker& w, DevSlot& d) {
   LBF_HIP_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
   LBF_HIP_TRY(hipMalloc((void**)&d.d_out, w.desc_cap * 20));
   LBF_HIP_TRY(host_alloc(w, (void**)&d.h_out, w.desc_cap * 20));
+  LBF_HIP_TRY(host_alloc(w, (void**)&d.h_hdr, w.hdr_cap));
   if (w.slot_bytes) LBF_HIP_TRY(hipMalloc((void**)&d.d_buf, w.hdr_cap + w.slot_bytes));
   d.ok.assign(w.desc_cap, 0);
   return LBF_OK;
@@ -370,6 +376,7 @@ void dev_slot_free(DevSlot& d) {
   if (d.d_buf) (void)hipFree(d.d_buf);
   if (d.d_out) (void)hipFree(d.d_out);
   if (d.h_out) (void)hipHostFree(d.h_out);
+  if (d.h_hdr) (void)hipHostFree(d.h_hdr);
   if (d.stream) (void)hipStreamDestroy(d.stream);
   d = DevSlot{};
 }
@@ -381,22 +388,32 @@ void dev_slot_free(DevSlot& d) {
 constexpr uint64_t kSlotStep = 8ull << 20;
 
 int ensure_slot_bytes(Worker& w, uint64_t need) {
-  need = std::min(w.slot_max, (std::max(need, kSlotStep) + kSlotStep - 1) / kSlotStep * kSlotStep);
-  if (need <= w.slot_bytes) return LBF_OK;
-  for (DevSlot& d : w.dev) {
-    LBF_HIP_TRY(hipStreamSynchronize(d.stream));
-    if (d.d_buf) (void)hipFree(d.d_buf);
-    d.d_buf = nullptr;
+  auto round = [](uint64_t x, uint64_t cap) {
+    return std::min(cap, (std::max(x, kSlotStep) + kSlotStep - 1) / kSlotStep * kSlotStep);
+  };
+  const uint64_t dev_need = round(need, w.slot_max);
+  const uint64_t pin_need = round(std::min(need, w.pin_max), w.pin_max);
+  if (dev_need > w.slot_bytes) {
+    for (DevSlot& d : w.dev) {
+      LBF_HIP_TRY(hipStreamSynchronize(d.stream));
+      if (d.d_buf) (void)hipFree(d.d_buf);
+      d.d_buf = nullptr;
+    }
+    w.slot_bytes = 0;
+    for (DevSlot& d : w.dev) LBF_HIP_TRY(hipMalloc((void**)&d.d_buf, w.hdr_cap + dev_need));
+    w.slot_bytes = dev_need;
   }
-  for (HostSlot& h : w.host) {
-    if (h.h_buf) (void)hipHostFree(h.h_buf);
-    h.h_buf = nullptr;
-    h.in_flight = false;
+  if (pin_need > w.pin_bytes) {
+    for (DevSlot& d : w.dev) LBF_HIP_TRY(hipStreamSynchronize(d.stream));  // no H2D reads a host slot
+    for (HostSlot& h : w.host) {
+      if (h.h_buf) (void)hipHostFree(h.h_buf);
+      h.h_buf = nullptr;
+      h.in_flight = false;
+    }
+    w.pin_bytes = 0;
+    for (HostSlot& h : w.host) LBF_HIP_TRY(host_alloc(w, (void**)&h.h_buf, pin_need));
+    w.pin_bytes = pin_need;
   }
-  w.slot_bytes = 0;
-  for (DevSlot& d : w.dev) LBF_HIP_TRY(hipMalloc((void**)&d.d_buf, w.hdr_cap + need));
-  for (HostSlot& h : w.host) LBF_HIP_TRY(host_alloc(w, (void**)&h.h_buf, w.hdr_cap + need));
-  w.slot_bytes = need;
   return LBF_OK;
 }
 
@@ -436,6 +453,7 @@ int worker_init(Worker& w, int device, int index) {
   w.device = device;
   w.index = index;
   w.slot_max = std::max<uint64_t>(env_u64("LBF_SLOT_MB", 512) << 20, 1ull << 20);
+  w.pin_max = std::max<uint64_t>(env_u64("LBF_PIN_MB", 128) << 20, 1ull << 20);
   w.dev_budget = std::max<uint64_t>(env_u64("LBF_DEVICE_STAGING_MB", 16384) << 20, 1ull << 20);
   // Three pinned slots keep the PCIe link busy: with two, staging group g+2
   // waits for group g's H2D, so the link idles while the host copies.
@@ -772,15 +790,58 @@ int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
       rc = fail(LBF_ERR_HIP, "injected fault (LBF_TEST_FAULT_GROUP) at group " + std::to_string(group - 1));
       break;
     }
-    HostSlot& h = w.host[hcur];
-    if (h.in_flight && !hip_ok(hipEventSynchronize(h.copied), "hipEventSynchronize")) break;  // its last H2D is done
-    h.in_flight = false;
     const uint64_t cnt = j - i;
     const uint64_t hdr = header_bytes(cnt);
-    uint64_t* h_off = reinterpret_cast<uint64_t*>(h.h_buf);
-    uint32_t* h_size = reinterpret_cast<uint32_t*>(h.h_buf + 8 * cnt);
-    uint8_t* h_exp = h.h_buf + 12 * cnt;
-    read_runs(job.src, runs, h.h_buf + hdr, w.cpus);
+    // The batch's bytes, [0, cursor) of its data area, go through the host
+    // ring: in one [header | data] copy when they fit a host slot, else in
+    // pieces of pin_bytes followed by the header from the slot's own pinned
+    // header buffer.  A run cut by a piece boundary is read in parts; once a
+    // part comes back short (EOF), the rest of that run is unavailable.
+    const bool single = hdr + cursor <= w.pin_bytes;
+    const uint64_t data_off = single ? hdr : w.hdr_cap;
+    uint8_t* h_header = nullptr;
+    for (Run& r : runs) r.avail = 0;
+    std::vector<bool> cut_short(runs.size(), false);
+    size_t first_run = 0;
+    for (uint64_t pstart = 0; (pstart < cursor || (single && pstart == 0)) && rc == LBF_OK;) {
+      const uint64_t room = single ? cursor : w.pin_bytes;
+      const uint64_t pend = std::min(cursor, pstart + room);
+      HostSlot& h = w.host[hcur];
+      if (h.in_flight && !hip_ok(hipEventSynchronize(h.copied), "hipEventSynchronize")) break;  // its last H2D is done
+      h.in_flight = false;
+      uint8_t* piece = h.h_buf + (single ? hdr : 0);
+      std::vector<Run> parts;
+      std::vector<size_t> part_of;
+      while (first_run < runs.size() && runs[first_run].dst + runs[first_run].len <= pstart) ++first_run;
+      for (size_t r = first_run; r < runs.size() && runs[r].dst < pend; ++r) {
+        const uint64_t a0 = std::max(runs[r].dst, pstart), a1 = std::min(runs[r].dst + runs[r].len, pend);
+        if (a1 <= a0 || cut_short[r]) continue;
+        parts.push_back(Run{runs[r].src + (a0 - runs[r].dst), a1 - a0, a0 - pstart, 0, runs[r].file});
+        part_of.push_back(r);
+      }
+      read_runs(job.src, parts, piece, w.cpus);
+      for (size_t q = 0; q < parts.size(); ++q) {
+        Run& r = runs[part_of[q]];
+        r.avail += parts[q].avail;
+        if (parts[q].avail < parts[q].len) cut_short[part_of[q]] = true;
+      }
+      if (single) {
+        h_header = h.h_buf;  // the header is written below, then header + data go in one copy
+        break;
+      }
+      if (!hip_ok(hipMemcpyAsync(s.d_buf + data_off + pstart, piece, pend - pstart, hipMemcpyHostToDevice, s.stream),
+                  "hipMemcpyAsync(H2D)") ||
+          !hip_ok(hipEventRecord(h.copied, s.stream), "hipEventRecord"))
+        break;
+      h.in_flight = true;
+      hcur = (hcur + 1) % (int)w.host.size();
+      pstart = pend;
+    }
+    if (rc) break;
+    if (!single) h_header = s.h_hdr;
+    uint64_t* h_off = reinterpret_cast<uint64_t*>(h_header);
+    uint32_t* h_size = reinterpret_cast<uint32_t*>(h_header + 8 * cnt);
+    uint8_t* h_exp = h_header + 12 * cnt;
     for (uint64_t q = 0; q < cnt; ++q) {
       const uint64_t k = order(i + q), o = job.offsets[k], sz = job.sizes[k];
       const uint32_t r = run_of[q];
@@ -794,14 +855,23 @@ int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
       h_size[q] = s.ok[q] ? (uint32_t)sz : 0;
       if (job.expected) memcpy(h_exp + 20 * q, job.expected + 20 * k, 20);
     }
-    if (!hip_ok(hipMemcpyAsync(s.d_buf, h.h_buf, hdr + cursor, hipMemcpyHostToDevice, s.stream), "hipMemcpyAsync(H2D)") ||
-        !hip_ok(hipEventRecord(h.copied, s.stream), "hipEventRecord"))
-      break;
-    h.in_flight = true;
+    {
+      // header (+ data, for a single-piece batch) after the pieces, on the same stream
+      HostSlot& h = w.host[hcur];
+      const uint64_t bytes = single ? hdr + cursor : hdr;
+      if (!hip_ok(hipMemcpyAsync(s.d_buf, h_header, bytes, hipMemcpyHostToDevice, s.stream), "hipMemcpyAsync(H2D)"))
+        break;
+      if (single) {
+        if (!hip_ok(hipEventRecord(h.copied, s.stream), "hipEventRecord")) break;
+        h.in_flight = true;
+        hcur = (hcur + 1) % (int)w.host.size();
+      }
+    }
     const uint64_t* d_off = reinterpret_cast<const uint64_t*>(s.d_buf);
     const uint32_t* d_size = reinterpret_cast<const uint32_t*>(s.d_buf + 8 * cnt);
-    if (job.expected) rc = lbf_sha1_launch(s.d_buf + hdr, d_off, d_size, cnt, nullptr, s.d_buf + 12 * cnt, s.d_out, s.stream);
-    else rc = lbf_sha1_launch(s.d_buf + hdr, d_off, d_size, cnt, s.d_out, nullptr, nullptr, s.stream);
+    if (job.expected)
+      rc = lbf_sha1_launch(s.d_buf + data_off, d_off, d_size, cnt, nullptr, s.d_buf + 12 * cnt, s.d_out, s.stream);
+    else rc = lbf_sha1_launch(s.d_buf + data_off, d_off, d_size, cnt, s.d_out, nullptr, nullptr, s.stream);
     if (rc) break;
     if (!hip_ok(hipMemcpyAsync(s.h_out, s.d_out, cnt * (job.expected ? 1 : 20), hipMemcpyDeviceToHost, s.stream),
                 "hipMemcpyAsync(D2H)"))
@@ -810,7 +880,6 @@ int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
     s.g_begin = i;
     s.g_end = j;
     cur = (cur + 1) % (int)w.dev.size();
-    hcur = (hcur + 1) % (int)w.host.size();
     i = j;
   }
   // drain, on every path (every H2D ran on a device slot's stream, so this also

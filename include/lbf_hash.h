@@ -61,9 +61,11 @@ const char* lbf_last_error(void);
 int lbf_device_count(int* out_count);
 /* device_mask bit d selects device d; 0 selects every visible device.
  * Fails with LBF_ERR_NO_DEVICE when no GPU is visible.  Host-path staging,
- * read at creation: LBF_SLOTS slots per worker (2..8, default 3), each grown
- * on demand up to LBF_SLOT_MB MiB (default 512); LBF_COPY_THREADS host copy
- * threads (default 8).  Pinned staging is allocated on the GPU's NUMA node and
+ * read at creation: batches of up to LBF_SLOT_MB MiB (default 512) in HBM
+ * device slots (as many as one chain's duration at PCIe rate needs, within
+ * LBF_DEVICE_STAGING_MB, default 16384), fed through LBF_SLOTS pinned host
+ * slots per worker (2..8, default 3) of up to LBF_PIN_MB MiB (default 128),
+ * all grown on demand; LBF_COPY_THREADS host copy threads (default 8).  Pinned staging is allocated on the GPU's NUMA node and
  * the copy threads run on that node's CPUs (LBF_NUMA=0 turns this off). */
 int lbf_ctx_create(uint32_t device_mask, lbf_ctx** out_ctx);
 void lbf_ctx_destroy(lbf_ctx* ctx);
