@@ -419,31 +419,37 @@ int ensure_slot_bytes(Worker& w, uint64_t need) {
 
 // Device slots for a job whose longest staged chunk is `largest` bytes: enough
 // to keep ≈50 GB/s of H2D going for one chain's duration (≈1 µs per 64-byte
-// block, conservatively), at least one per host slot, at most the HBM budget.
+// block, conservatively), never more than the process's hardware queues
+// (GPU_MAX_HW_QUEUES, HIP's default 4): streams beyond that share a queue, and
+// a batch's copies would then wait behind another slot's long kernel.  At
+// least kDevSlots, at most the HBM budget.
+constexpr uint64_t kDevSlots = 3;
+
 int ensure_dev_slots(Worker& w, uint64_t largest, uint64_t groups) {
+  static const uint64_t hw_queues = (uint64_t)std::max(2L, std::min(32L, env_long("GPU_MAX_HW_QUEUES", 4)));
   const double chain_us = ((double)largest / 64.0 + 2.0) * 1.0;
   const uint64_t in_flight = (uint64_t)(50e3 * chain_us);  // bytes at 50 GB/s
   const uint64_t per = w.hdr_cap + w.slot_bytes;
   uint64_t want = (in_flight + w.slot_bytes - 1) / std::max<uint64_t>(1, w.slot_bytes) + 1;
   want = std::min<uint64_t>(want, groups);
   want = std::min<uint64_t>(want, std::max<uint64_t>(1, w.dev_budget / per));
-  want = std::min<uint64_t>(32, std::max<uint64_t>(want, w.host.size()));
+  want = std::min<uint64_t>(hw_queues, std::max<uint64_t>(want, std::min(kDevSlots, hw_queues)));
   while (w.dev.size() < want) {
     w.dev.emplace_back();
     if (int rc = dev_slot_init(w, w.dev.back())) {
       std::string msg = lbf_last_error();
       dev_slot_free(w.dev.back());
       w.dev.pop_back();
-      if (w.dev.size() >= w.host.size()) break;  // fewer slots in flight: slower, not wrong
+      if (w.dev.size() >= kDevSlots) break;  // fewer slots in flight: slower, not wrong
       return fail(rc, msg);
     }
   }
   return LBF_OK;
 }
 
-// After a job, give back the device slots beyond one per host slot.
+// After a job, give back the device slots beyond kDevSlots.
 void trim_dev_slots(Worker& w) {
-  while (w.dev.size() > w.host.size()) {
+  while (w.dev.size() > kDevSlots) {
     dev_slot_free(w.dev.back());
     w.dev.pop_back();
   }
@@ -470,7 +476,7 @@ int worker_init(Worker& w, int device, int index) {
     w.cpus = node_cpus_allowed(w.numa_node);
   }
   for (HostSlot& h : w.host) LBF_HIP_TRY(hipEventCreateWithFlags(&h.copied, hipEventDisableTiming));
-  w.dev.resize(w.host.size());
+  w.dev.resize(kDevSlots);
   for (DevSlot& d : w.dev)
     if (int rc = dev_slot_init(w, d)) return rc;
   return LBF_OK;
