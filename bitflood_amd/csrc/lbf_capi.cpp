@@ -387,11 +387,11 @@ void dev_slot_free(DevSlot& d) {
 // should not pay.  Slots grow, never shrink, in 8 MiB steps up to slot_max.
 constexpr uint64_t kSlotStep = 8ull << 20;
 
-int ensure_slot_bytes(Worker& w, uint64_t need) {
+int ensure_slot_bytes(Worker& w, uint64_t need, uint64_t dev_cap) {
   auto round = [](uint64_t x, uint64_t cap) {
     return std::min(cap, (std::max(x, kSlotStep) + kSlotStep - 1) / kSlotStep * kSlotStep);
   };
-  const uint64_t dev_need = round(need, w.slot_max);
+  const uint64_t dev_need = round(need, dev_cap);
   const uint64_t pin_need = round(std::min(need, w.pin_max), w.pin_max);
   if (dev_need > w.slot_bytes) {
     for (DevSlot& d : w.dev) {
@@ -447,11 +447,20 @@ int ensure_dev_slots(Worker& w, uint64_t largest, uint64_t groups) {
   return LBF_OK;
 }
 
-// After a job, give back the device slots beyond kDevSlots.
+// After a job, give back the device slots beyond kDevSlots, and the HBM of
+// batches grown past LBF_SLOT_MB for long chains (the next job sizes its own).
 void trim_dev_slots(Worker& w) {
   while (w.dev.size() > kDevSlots) {
     dev_slot_free(w.dev.back());
     w.dev.pop_back();
+  }
+  if (w.slot_bytes > w.slot_max) {
+    for (DevSlot& d : w.dev) {
+      (void)hipStreamSynchronize(d.stream);  // drained already; errors were reported by the job
+      if (d.d_buf) (void)hipFree(d.d_buf);
+      d.d_buf = nullptr;
+    }
+    w.slot_bytes = 0;
   }
 }
 
@@ -733,9 +742,18 @@ int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
         open = true;
       }
     }
-    const uint64_t per = bytes <= kSplitMin ? bytes : std::max({kSplitMin, (bytes + 3) / 4, largest});
+    uint64_t per = bytes <= kSplitMin ? bytes : std::max({kSplitMin, (bytes + 3) / 4, largest});
+    per = std::min(per, w.slot_max);
+    // Long chains: a batch's kernel lasts one chain (≈1 µs per 64-byte block)
+    // and at most ~4 batches are in flight (the hardware queues, see
+    // ensure_dev_slots), so batches grow until three of them hold a chain's
+    // worth of PCIe time -- beyond LBF_SLOT_MB, within a quarter of the HBM
+    // budget and a quarter of the job.
+    const uint64_t in_flight = (uint64_t)(50e3 * ((double)largest / 64.0 + 2.0));
+    const uint64_t dev_cap = std::max(w.slot_max, w.dev_budget / 4);
+    if (in_flight > 3 * per) per = std::max(per, std::min({in_flight / 3, dev_cap, (bytes + 3) / 4}));
     if (end > begin) {
-      if (int rc = ensure_slot_bytes(w, std::min(per, w.slot_max) + 16)) return rc;  // nothing pending yet
+      if (int rc = ensure_slot_bytes(w, per + 16, dev_cap)) return rc;  // nothing pending yet
       const uint64_t groups = bytes / std::max<uint64_t>(1, w.slot_bytes) + 2;
       if (int rc = ensure_dev_slots(w, largest, groups)) return rc;
     }
