@@ -753,7 +753,8 @@ int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
     const uint64_t dev_cap = std::max(w.slot_max, w.dev_budget / 4);
     if (in_flight > 3 * per) per = std::max(per, std::min({in_flight / 3, dev_cap, (bytes + 3) / 4}));
     if (end > begin) {
-      if (int rc = ensure_slot_bytes(w, per + 16, dev_cap)) return rc;  // nothing pending yet
+      // (LBF_SLOT_MB stays the cap unless the long-chain rule raised the batch)
+      if (int rc = ensure_slot_bytes(w, per + 16, per > w.slot_max ? dev_cap : w.slot_max)) return rc;
       const uint64_t groups = bytes / std::max<uint64_t>(1, w.slot_bytes) + 2;
       if (int rc = ensure_dev_slots(w, largest, groups)) return rc;
     }
