@@ -226,7 +226,7 @@ constexpr int kPx5B1 = 14, kPx5B1At = 7;   // raw + pairs 0..13 first; 14..23 af
 constexpr int kPx5B2 = 24, kPx5B2At = 19;  // pairs 24..31 after round 40
 
 struct Px5Sched {
-  uint4 raw[4];  // words 0..15, little-endian
+  uint4 raw[4];  // words 0..15, big-endian (swapped by the producer)
   uint2 v[32];   // words 16..79
 };
 
@@ -248,10 +248,10 @@ __device__ __forceinline__ void px5_compress(Digest& s, const Px5Sched& cur, Px5
   uint32_t a = s.h[0], b = s.h[1], c = s.h[2], d = s.h[3], e = s.h[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    px4_round<kKFrom>(4 * j + 0, a, b, c, d, e, bswap(cur.raw[j].x), K);
-    px4_round<kKFrom>(4 * j + 1, a, b, c, d, e, bswap(cur.raw[j].y), K);
-    px4_round<kKFrom>(4 * j + 2, a, b, c, d, e, bswap(cur.raw[j].z), K);
-    px4_round<kKFrom>(4 * j + 3, a, b, c, d, e, bswap(cur.raw[j].w), K);
+    px4_round<kKFrom>(4 * j + 0, a, b, c, d, e, cur.raw[j].x, K);
+    px4_round<kKFrom>(4 * j + 1, a, b, c, d, e, cur.raw[j].y, K);
+    px4_round<kKFrom>(4 * j + 2, a, b, c, d, e, cur.raw[j].z, K);
+    px4_round<kKFrom>(4 * j + 3, a, b, c, d, e, cur.raw[j].w, K);
   }
 #pragma unroll
   for (int q = 0; q < 32; ++q) {
@@ -298,19 +298,19 @@ __device__ __forceinline__ void px5_produce(uint4* ring, uint32_t raw_lds, const
   uint4* raw = ring + kPx4Ring * kPx5SlotU4 + (step % kPx5Raw) * kPcRawU4 + lane;
   if (c.aligned && step < c.nfull) {
     block_from_vec(w, raw[0], raw[kPcLanes], raw[2 * kPcLanes], raw[3 * kPcLanes]);
+  } else if (step < c.nfull) {
+    load_words_any(w, c.src + 64ull * step, 64);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) w[k] = bswap(w[k]);
   } else {
-    if (step < c.nfull) {
-      load_words_any(w, c.src + 64ull * step, 64);
-#pragma unroll
-      for (int k = 0; k < 16; ++k) w[k] = bswap(w[k]);
-    } else {
-      final_block(w, c.src + 64ull * c.nfull, c.size & 63u, c.size, step != c.nfull);
-    }
-    // the consumer reads words 0..15 of every step from the raw slot
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      raw[j * kPcLanes] = make_uint4(bswap(w[4 * j]), bswap(w[4 * j + 1]), bswap(w[4 * j + 2]), bswap(w[4 * j + 3]));
+    final_block(w, c.src + 64ull * c.nfull, c.size & 63u, c.size, step != c.nfull);
   }
+  // The consumer reads words 0..15 of every step from the raw slot: the
+  // producer leaves them there byte-swapped (big-endian), so the consumer,
+  // the side that bounds pcx5, issues no v_perm (4 KiB more of producer
+  // stores, which it has the slack for: DESIGN.md §4.3f).
+#pragma unroll
+  for (int j = 0; j < 4; ++j) raw[j * kPcLanes] = make_uint4(w[4 * j], w[4 * j + 1], w[4 * j + 2], w[4 * j + 3]);
   px5_dma(c, step + kPx5Raw - 2, raw_lds);  // into the slot of block step - 2, read before barrier step - 2
   expand_store_from16<kKFrom>(w, reinterpret_cast<uint2*>(ring + (step % kPx4Ring) * kPx5SlotU4) + lane, kPcLanes);
 }
