@@ -207,11 +207,13 @@ void launch_pcx4(const ChunkParams& p, hipStream_t stream) {
 // pcx4 is producer-bound (≈2,170 cycles per step); ≈690 of a producer's
 // cycles are its 20 KiB of stores.  Words 0..15 of a step are the chunk's own
 // 64 bytes, already in LDS from the DMA, so the consumer reads them there
-// (4 ds_read_b128 of the raw slot) and swaps their bytes itself (16 v_perm);
-// the producer stores only words 16..79 (16 KiB).  The consumer's load count
-// stays at 20 instructions per step.  For final and misaligned blocks the
-// producer writes the little-endian words it built into the raw slot, so the
-// consumer's read is the same for every step.
+// (4 ds_read_b128 of the raw slot); the producer stores words 16..79 (16 KiB)
+// and writes words 0..15 back over the raw block byte-swapped (4 KiB), so the
+// consumer issues no v_perm: pcx5 is consumer-bound, and moving the 16 swaps
+// to the producer took C4 from 14.00 to 13.69 ms (profiles/r02/px5_be).  For
+// final and misaligned blocks those words are the ones the producer built, so
+// the consumer's read is the same for every step.  The consumer's load count
+// stays at 20 instructions per step.
 //
 // Raw slots: 6 per pair, block s in slot s % 6.  The consumer reads block s in
 // interval s (like the words of step s), so the slot is refilled only when
@@ -414,7 +416,10 @@ __global__ void __launch_bounds__(256) sha1_pcx5_kernel(ChunkParams p) {
 // 2 % slower, 48 and 56 within 0.5 % (profiles/r01/sweep_v9_pcx5_k40_k48.log,
 // sweep_pcx5_k48_k56_k64.log); 72 ran 1.5 % and 80 (no K in the producer)
 // 5 % slower (sweep_pcx5_k64_k72_k80.log).
-constexpr int kPx5KFrom = 64;
+#ifndef LBF_PX5_KFROM  // A/B builds only (tools/px5_ab.sh)
+#define LBF_PX5_KFROM 64
+#endif
+constexpr int kPx5KFrom = LBF_PX5_KFROM;
 
 template <int kKFrom>
 void launch_pcx5(const ChunkParams& p, hipStream_t stream) {
