@@ -58,8 +58,9 @@ PC2_CYCLES_PER_BLOCK = 80 * 5 * 4.09
 PC_CYCLES_PER_BLOCK = 80 * 23.2
 #  pcx4 consumer: rounds 0..39 in the two-add3 form, 40..79 with W+K
 PCX4_CYCLES_PER_BLOCK = 40 * 23.2 + 40 * 5 * 4.09
-#  pcx5 consumer: rounds 0..63 in the two-add3 form, 64..79 with W+K, 16 byte swaps
-PCX5_CYCLES_PER_BLOCK = 64 * 23.2 + 16 * 5 * 4.09 + 16 * 4.09
+#  pcx5 consumer: rounds 0..63 in the two-add3 form, 64..79 with W+K (the producer
+#    byte-swaps words 0..15 since round 2)
+PCX5_CYCLES_PER_BLOCK = 64 * 23.2 + 16 * 5 * 4.09
 FUSED_VALU_PER_BLOCK = 613
 
 
