@@ -8,6 +8,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "libBitFlood/Encoder.H"
@@ -68,6 +69,36 @@ int main(int argc, char** argv) {
     std::string one;
     Encoder::Base64Encode(buf.data() + offs[i], sizes[i], one);
     CHECK(hs[i] == one);
+  }
+
+  // Base64Encode from several threads at once, as the reference's reentrant
+  // call allows (a stack hasher per call, Encoder.cpp:107-120): each thread's
+  // strings equal the ones computed one call at a time above
+  {
+    std::vector<std::string> one(64);
+    std::vector<U32> at(64), len(64);
+    for (U32 k = 0; k < 64; ++k) {
+      at[k] = (k * 7919u) % 500000u;
+      len[k] = (k * 104729u) % 300000u;
+      Encoder::Base64Encode(buf.data() + at[k], len[k], one[k]);
+    }
+    std::vector<int> bad(8, 0);
+    std::vector<std::thread> th;
+    for (int t = 0; t < 8; ++t)
+      th.emplace_back([&, t] {
+        for (int rep = 0; rep < 3; ++rep)
+          for (U32 k = (U32)t; k < 64; k += 2) {
+            std::string s2;
+            if (Encoder::Base64Encode(buf.data() + at[k], len[k], s2) != Error::NO_ERROR_LBF || s2 != one[k]) ++bad[t];
+          }
+        V_String many;
+        std::vector<U64> o(at.begin(), at.end());
+        if (Encoder::Base64EncodeBatch(buf.data(), buf.size(), o.data(), len.data(), 64, many) != Error::NO_ERROR_LBF ||
+            many != one)
+          ++bad[t];
+      });
+    for (auto& x : th) x.join();
+    for (int t = 0; t < 8; ++t) CHECK(bad[t] == 0);
   }
 
   // EncodeFile -> Flood: seeder read-verify, receiver accept/reject
