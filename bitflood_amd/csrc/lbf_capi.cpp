@@ -22,10 +22,14 @@
 #include <algorithm>
 #include <atomic>
 #include <cctype>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <mutex>
+#include <new>
+#include <stdexcept>
 #include <string>
+#include <system_error>
 #include <thread>
 #include <vector>
 
@@ -50,9 +54,25 @@ int hip_fail(hipError_t e, const char* what) {
               std::string(what) + ": " + hipGetErrorString(e));
 }
 
+// Nothing is thrown across the C ABI: a host allocation that
+// fails, or a thread that cannot be started, inside a call becomes a status.
+template <class F>
+int guarded(F&& f) {
+  try {
+    return f();
+  } catch (const std::bad_alloc&) {
+    return fail(LBF_ERR_NOMEM, "host allocation failed");
+  } catch (const std::system_error& e) {
+    return fail(LBF_ERR_NOMEM, std::string("host resources: ") + e.what());
+  } catch (const std::exception& e) {
+    return fail(LBF_ERR_INVALID, std::string("internal error: ") + e.what());
+  }
+}
+
 }  // namespace lbf
 
 using lbf::fail;
+using lbf::guarded;
 using lbf::hip_fail;
 
 // ---------------------------------------------------------------------------
@@ -573,15 +593,26 @@ void read_runs(const Source& src, std::vector<Run>& runs, uint8_t* data, const s
   for (size_t k = 0; k < runs.size(); ++k)
     for (uint64_t a = 0; a < runs[k].len; a += step) pieces.push_back({k, a, std::min(step, runs[k].len - a), 0});
   std::atomic<size_t> next{0};
+  auto pull = [&] {
+    for (size_t q; (q = next++) < pieces.size();) {
+      Piece& pc = pieces[q];
+      pc.got = src.read_serial(data + runs[pc.run].dst + pc.at, runs[pc.run].file, runs[pc.run].src + pc.at, pc.len);
+    }
+  };
+  // parts - 1 helpers plus the calling thread (already bound by its worker);
+  // a helper that cannot be started leaves its pieces to the others
   std::vector<std::thread> th;
-  for (uint64_t t = 0; t < parts; ++t)
-    th.emplace_back([&] {
-      bind_thread(cpus);
-      for (size_t q; (q = next++) < pieces.size();) {
-        Piece& pc = pieces[q];
-        pc.got = src.read_serial(data + runs[pc.run].dst + pc.at, runs[pc.run].file, runs[pc.run].src + pc.at, pc.len);
-      }
-    });
+  for (uint64_t t = 1; t < parts; ++t) {
+    try {
+      th.emplace_back([&] {
+        bind_thread(cpus);
+        pull();
+      });
+    } catch (const std::system_error&) {
+      break;
+    }
+  }
+  pull();
   for (auto& t : th) t.join();
   // a run's readable prefix: its pieces in order up to the first short one
   std::vector<bool> short_seen(runs.size(), false);
@@ -770,142 +801,150 @@ int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
     rc = hip_fail(e, what);
     return false;
   };
-  while (i < end && rc == LBF_OK) {
-    if ((uint64_t)job.sizes[order(i)] + 15 > w.slot_bytes) {
-      for (DevSlot& s : w.dev) {
-        if (!hip_ok(hipStreamSynchronize(s.stream), "hipStreamSynchronize")) break;
-        if ((rc = finalize(job, order, s))) break;
-      }
-      if (rc == LBF_OK) rc = run_oversize(w, job, order(i));
-      ++i;
-      continue;
-    }
-    // group [i, j) of positions, packed as runs
-    runs.clear();
-    run_of.clear();
-    uint64_t cursor = 0, j = i;
-    while (j < end && j - i < w.desc_cap) {
-      const uint64_t k = order(j), o = job.offsets[k], sz = job.sizes[k];
-      if (sz == 0) {  // empty chunks take no bytes
-        run_of.push_back(UINT32_MAX);
-        ++j;
+  // An exception in the loop (a host allocation) must not skip the drain
+  // below: groups may be in flight.
+  try {
+    while (i < end && rc == LBF_OK) {
+      if ((uint64_t)job.sizes[order(i)] + 15 > w.slot_bytes) {
+        for (DevSlot& s : w.dev) {
+          if (!hip_ok(hipStreamSynchronize(s.stream), "hipStreamSynchronize")) break;
+          if ((rc = finalize(job, order, s))) break;
+        }
+        if (rc == LBF_OK) rc = run_oversize(w, job, order(i));
+        ++i;
         continue;
       }
-      if (sz + 15 > w.slot_bytes) break;  // oversize: the next group starts with it
-      Run* r = runs.empty() ? nullptr : &runs.back();
-      if (r && r->file == job.file(k) && o >= r->src && o <= r->src + r->len + kJoinGap) {
-        const uint64_t new_len = std::max(r->len, o + sz - r->src);
-        if (r->dst + new_len > w.slot_bytes) break;
-        r->len = new_len;
-        cursor = r->dst + new_len;
-      } else {
-        const uint64_t p = cursor + ((o - cursor) & 15u);
-        if (p + sz > w.slot_bytes) break;
-        runs.push_back(Run{o, sz, p, 0, job.file(k)});
-        cursor = p + sz;
+      // group [i, j) of positions, packed as runs
+      runs.clear();
+      run_of.clear();
+      uint64_t cursor = 0, j = i;
+      while (j < end && j - i < w.desc_cap) {
+        const uint64_t k = order(j), o = job.offsets[k], sz = job.sizes[k];
+        if (sz == 0) {  // empty chunks take no bytes
+          run_of.push_back(UINT32_MAX);
+          ++j;
+          continue;
+        }
+        if (sz + 15 > w.slot_bytes) break;  // oversize: the next group starts with it
+        Run* r = runs.empty() ? nullptr : &runs.back();
+        if (r && r->file == job.file(k) && o >= r->src && o <= r->src + r->len + kJoinGap) {
+          const uint64_t new_len = std::max(r->len, o + sz - r->src);
+          if (r->dst + new_len > w.slot_bytes) break;
+          r->len = new_len;
+          cursor = r->dst + new_len;
+        } else {
+          const uint64_t p = cursor + ((o - cursor) & 15u);
+          if (p + sz > w.slot_bytes) break;
+          runs.push_back(Run{o, sz, p, 0, job.file(k)});
+          cursor = p + sz;
+        }
+        run_of.push_back((uint32_t)(runs.size() - 1));
+        ++j;
       }
-      run_of.push_back((uint32_t)(runs.size() - 1));
-      ++j;
-    }
-    DevSlot& s = w.dev[cur];
-    if (!hip_ok(hipStreamSynchronize(s.stream), "hipStreamSynchronize")) break;
-    if ((rc = finalize(job, order, s))) break;
-    if (group++ == w.fault_group) {
-      w.fault_group = -1;
-      rc = fail(LBF_ERR_HIP, "injected fault (LBF_TEST_FAULT_GROUP) at group " + std::to_string(group - 1));
-      break;
-    }
-    const uint64_t cnt = j - i;
-    const uint64_t hdr = header_bytes(cnt);
-    // The batch's bytes, [0, cursor) of its data area, go through the host
-    // ring: in one [header | data] copy when they fit a host slot, else in
-    // pieces of pin_bytes followed by the header from the slot's own pinned
-    // header buffer.  A run cut by a piece boundary is read in parts; once a
-    // part comes back short (EOF), the rest of that run is unavailable.
-    const bool single = hdr + cursor <= w.pin_bytes;
-    const uint64_t data_off = single ? hdr : w.hdr_cap;
-    uint8_t* h_header = nullptr;
-    for (Run& r : runs) r.avail = 0;
-    std::vector<bool> cut_short(runs.size(), false);
-    size_t first_run = 0;
-    for (uint64_t pstart = 0; (pstart < cursor || (single && pstart == 0)) && rc == LBF_OK;) {
-      const uint64_t room = single ? cursor : w.pin_bytes;
-      const uint64_t pend = std::min(cursor, pstart + room);
-      HostSlot& h = w.host[hcur];
-      if (h.in_flight && !hip_ok(hipEventSynchronize(h.copied), "hipEventSynchronize")) break;  // its last H2D is done
-      h.in_flight = false;
-      uint8_t* piece = h.h_buf + (single ? hdr : 0);
-      std::vector<Run> parts;
-      std::vector<size_t> part_of;
-      while (first_run < runs.size() && runs[first_run].dst + runs[first_run].len <= pstart) ++first_run;
-      for (size_t r = first_run; r < runs.size() && runs[r].dst < pend; ++r) {
-        const uint64_t a0 = std::max(runs[r].dst, pstart), a1 = std::min(runs[r].dst + runs[r].len, pend);
-        if (a1 <= a0 || cut_short[r]) continue;
-        parts.push_back(Run{runs[r].src + (a0 - runs[r].dst), a1 - a0, a0 - pstart, 0, runs[r].file});
-        part_of.push_back(r);
-      }
-      read_runs(job.src, parts, piece, w.cpus);
-      for (size_t q = 0; q < parts.size(); ++q) {
-        Run& r = runs[part_of[q]];
-        r.avail += parts[q].avail;
-        if (parts[q].avail < parts[q].len) cut_short[part_of[q]] = true;
-      }
-      if (single) {
-        h_header = h.h_buf;  // the header is written below, then header + data go in one copy
+      DevSlot& s = w.dev[cur];
+      if (!hip_ok(hipStreamSynchronize(s.stream), "hipStreamSynchronize")) break;
+      if ((rc = finalize(job, order, s))) break;
+      if (group++ == w.fault_group) {
+        w.fault_group = -1;
+        rc = fail(LBF_ERR_HIP, "injected fault (LBF_TEST_FAULT_GROUP) at group " + std::to_string(group - 1));
         break;
       }
-      if (!hip_ok(hipMemcpyAsync(s.d_buf + data_off + pstart, piece, pend - pstart, hipMemcpyHostToDevice, s.stream),
-                  "hipMemcpyAsync(H2D)") ||
-          !hip_ok(hipEventRecord(h.copied, s.stream), "hipEventRecord"))
-        break;
-      h.in_flight = true;
-      hcur = (hcur + 1) % (int)w.host.size();
-      pstart = pend;
-    }
-    if (rc) break;
-    if (!single) h_header = s.h_hdr;
-    uint64_t* h_off = reinterpret_cast<uint64_t*>(h_header);
-    uint32_t* h_size = reinterpret_cast<uint32_t*>(h_header + 8 * cnt);
-    uint8_t* h_exp = h_header + 12 * cnt;
-    for (uint64_t q = 0; q < cnt; ++q) {
-      const uint64_t k = order(i + q), o = job.offsets[k], sz = job.sizes[k];
-      const uint32_t r = run_of[q];
-      // An empty chunk of an existing file is always readable, wherever it
-      // lies: the reference's fseek succeeds past EOF and fread of 0 bytes
-      // returns 0 (Flood.cpp:259-275); a file that cannot be opened leaves every
-      // chunk '0' (Flood.cpp:257).  Unreadable chunks must not be hashed from
-      // stale slot bytes: they get size 0 on the device (result discarded).
-      s.ok[q] = (r == UINT32_MAX ? job.src.exists(job.file(k)) : o + sz <= runs[r].src + runs[r].avail) ? 1 : 0;
-      h_off[q] = (r != UINT32_MAX && s.ok[q]) ? runs[r].dst + (o - runs[r].src) : 0;
-      h_size[q] = s.ok[q] ? (uint32_t)sz : 0;
-      if (job.expected) memcpy(h_exp + 20 * q, job.expected + 20 * k, 20);
-    }
-    {
-      // header (+ data, for a single-piece batch) after the pieces, on the same stream
-      HostSlot& h = w.host[hcur];
-      const uint64_t bytes = single ? hdr + cursor : hdr;
-      if (!hip_ok(hipMemcpyAsync(s.d_buf, h_header, bytes, hipMemcpyHostToDevice, s.stream), "hipMemcpyAsync(H2D)"))
-        break;
-      if (single) {
-        if (!hip_ok(hipEventRecord(h.copied, s.stream), "hipEventRecord")) break;
+      const uint64_t cnt = j - i;
+      const uint64_t hdr = header_bytes(cnt);
+      // The batch's bytes, [0, cursor) of its data area, go through the host
+      // ring: in one [header | data] copy when they fit a host slot, else in
+      // pieces of pin_bytes followed by the header from the slot's own pinned
+      // header buffer.  A run cut by a piece boundary is read in parts; once a
+      // part comes back short (EOF), the rest of that run is unavailable.
+      const bool single = hdr + cursor <= w.pin_bytes;
+      const uint64_t data_off = single ? hdr : w.hdr_cap;
+      uint8_t* h_header = nullptr;
+      for (Run& r : runs) r.avail = 0;
+      std::vector<bool> cut_short(runs.size(), false);
+      size_t first_run = 0;
+      for (uint64_t pstart = 0; (pstart < cursor || (single && pstart == 0)) && rc == LBF_OK;) {
+        const uint64_t room = single ? cursor : w.pin_bytes;
+        const uint64_t pend = std::min(cursor, pstart + room);
+        HostSlot& h = w.host[hcur];
+        if (h.in_flight && !hip_ok(hipEventSynchronize(h.copied), "hipEventSynchronize")) break;  // its last H2D is done
+        h.in_flight = false;
+        uint8_t* piece = h.h_buf + (single ? hdr : 0);
+        std::vector<Run> parts;
+        std::vector<size_t> part_of;
+        while (first_run < runs.size() && runs[first_run].dst + runs[first_run].len <= pstart) ++first_run;
+        for (size_t r = first_run; r < runs.size() && runs[r].dst < pend; ++r) {
+          const uint64_t a0 = std::max(runs[r].dst, pstart), a1 = std::min(runs[r].dst + runs[r].len, pend);
+          if (a1 <= a0 || cut_short[r]) continue;
+          parts.push_back(Run{runs[r].src + (a0 - runs[r].dst), a1 - a0, a0 - pstart, 0, runs[r].file});
+          part_of.push_back(r);
+        }
+        read_runs(job.src, parts, piece, w.cpus);
+        for (size_t q = 0; q < parts.size(); ++q) {
+          Run& r = runs[part_of[q]];
+          r.avail += parts[q].avail;
+          if (parts[q].avail < parts[q].len) cut_short[part_of[q]] = true;
+        }
+        if (single) {
+          h_header = h.h_buf;  // the header is written below, then header + data go in one copy
+          break;
+        }
+        if (!hip_ok(hipMemcpyAsync(s.d_buf + data_off + pstart, piece, pend - pstart, hipMemcpyHostToDevice, s.stream),
+                    "hipMemcpyAsync(H2D)") ||
+            !hip_ok(hipEventRecord(h.copied, s.stream), "hipEventRecord"))
+          break;
         h.in_flight = true;
         hcur = (hcur + 1) % (int)w.host.size();
+        pstart = pend;
       }
+      if (rc) break;
+      if (!single) h_header = s.h_hdr;
+      uint64_t* h_off = reinterpret_cast<uint64_t*>(h_header);
+      uint32_t* h_size = reinterpret_cast<uint32_t*>(h_header + 8 * cnt);
+      uint8_t* h_exp = h_header + 12 * cnt;
+      for (uint64_t q = 0; q < cnt; ++q) {
+        const uint64_t k = order(i + q), o = job.offsets[k], sz = job.sizes[k];
+        const uint32_t r = run_of[q];
+        // An empty chunk of an existing file is always readable, wherever it
+        // lies: the reference's fseek succeeds past EOF and fread of 0 bytes
+        // returns 0 (Flood.cpp:259-275); a file that cannot be opened leaves every
+        // chunk '0' (Flood.cpp:257).  Unreadable chunks must not be hashed from
+        // stale slot bytes: they get size 0 on the device (result discarded).
+        s.ok[q] = (r == UINT32_MAX ? job.src.exists(job.file(k)) : o + sz <= runs[r].src + runs[r].avail) ? 1 : 0;
+        h_off[q] = (r != UINT32_MAX && s.ok[q]) ? runs[r].dst + (o - runs[r].src) : 0;
+        h_size[q] = s.ok[q] ? (uint32_t)sz : 0;
+        if (job.expected) memcpy(h_exp + 20 * q, job.expected + 20 * k, 20);
+      }
+      {
+        // header (+ data, for a single-piece batch) after the pieces, on the same stream
+        HostSlot& h = w.host[hcur];
+        const uint64_t bytes = single ? hdr + cursor : hdr;
+        if (!hip_ok(hipMemcpyAsync(s.d_buf, h_header, bytes, hipMemcpyHostToDevice, s.stream), "hipMemcpyAsync(H2D)"))
+          break;
+        if (single) {
+          if (!hip_ok(hipEventRecord(h.copied, s.stream), "hipEventRecord")) break;
+          h.in_flight = true;
+          hcur = (hcur + 1) % (int)w.host.size();
+        }
+      }
+      const uint64_t* d_off = reinterpret_cast<const uint64_t*>(s.d_buf);
+      const uint32_t* d_size = reinterpret_cast<const uint32_t*>(s.d_buf + 8 * cnt);
+      if (job.expected)
+        rc = lbf_sha1_launch(s.d_buf + data_off, d_off, d_size, cnt, nullptr, s.d_buf + 12 * cnt, s.d_out, s.stream);
+      else rc = lbf_sha1_launch(s.d_buf + data_off, d_off, d_size, cnt, s.d_out, nullptr, nullptr, s.stream);
+      if (rc) break;
+      if (!hip_ok(hipMemcpyAsync(s.h_out, s.d_out, cnt * (job.expected ? 1 : 20), hipMemcpyDeviceToHost, s.stream),
+                  "hipMemcpyAsync(D2H)"))
+        break;
+      s.pending = true;
+      s.g_begin = i;
+      s.g_end = j;
+      cur = (cur + 1) % (int)w.dev.size();
+      i = j;
     }
-    const uint64_t* d_off = reinterpret_cast<const uint64_t*>(s.d_buf);
-    const uint32_t* d_size = reinterpret_cast<const uint32_t*>(s.d_buf + 8 * cnt);
-    if (job.expected)
-      rc = lbf_sha1_launch(s.d_buf + data_off, d_off, d_size, cnt, nullptr, s.d_buf + 12 * cnt, s.d_out, s.stream);
-    else rc = lbf_sha1_launch(s.d_buf + data_off, d_off, d_size, cnt, s.d_out, nullptr, nullptr, s.stream);
-    if (rc) break;
-    if (!hip_ok(hipMemcpyAsync(s.h_out, s.d_out, cnt * (job.expected ? 1 : 20), hipMemcpyDeviceToHost, s.stream),
-                "hipMemcpyAsync(D2H)"))
-      break;
-    s.pending = true;
-    s.g_begin = i;
-    s.g_end = j;
-    cur = (cur + 1) % (int)w.dev.size();
-    i = j;
+  } catch (const std::bad_alloc&) {
+    rc = fail(LBF_ERR_NOMEM, "host allocation failed while staging");
+  } catch (const std::system_error& e) {
+    rc = fail(LBF_ERR_NOMEM, std::string("host resources while staging: ") + e.what());
   }
   // drain, on every path (every H2D ran on a device slot's stream, so this also
   // completes every host slot's copy)
@@ -938,14 +977,20 @@ int run_job(lbf_ctx* ctx, const Job& job, uint64_t n) {
   std::vector<int> rcs(nw, LBF_OK);
   std::vector<std::string> errs(nw);
   std::vector<std::thread> th;
+  auto part = [&](size_t d, bool bind) {
+    if (bind) bind_thread(ctx->workers[d].cpus);
+    rcs[d] = guarded([&] { return worker_run(ctx->workers[d], job, n * d / nw, n * (d + 1) / nw); });
+    if (rcs[d]) errs[d] = lbf_last_error();
+  };
+  std::vector<size_t> inline_parts;  // workers whose thread could not be started run here, in turn
   for (size_t d = 0; d < nw; ++d) {
-    const uint64_t b = n * d / nw, e = n * (d + 1) / nw;
-    th.emplace_back([&, d, b, e] {
-      bind_thread(ctx->workers[d].cpus);
-      rcs[d] = worker_run(ctx->workers[d], job, b, e);
-      if (rcs[d]) errs[d] = lbf_last_error();
-    });
+    try {
+      th.emplace_back(part, d, true);
+    } catch (const std::system_error&) {
+      inline_parts.push_back(d);
+    }
   }
+  for (size_t d : inline_parts) part(d, false);
   for (auto& t : th) t.join();
   for (size_t d = 0; d < nw; ++d)
     if (rcs[d])
@@ -983,17 +1028,23 @@ extern "C" int lbf_ctx_create(uint32_t device_mask, lbf_ctx** out) {
   // per-worker staging and the error propagation of run_job run on a one-GPU
   // box exactly as they do with one worker per GPU on an 8-GPU node.
   const int per_dev = (int)std::max(1L, std::min(16L, env_long("LBF_WORKERS_PER_DEVICE", 1)));
-  lbf_ctx* ctx = new lbf_ctx();
-  for (int d = 0; d < ndev && d < 32; ++d) {
-    if (device_mask && !(device_mask & (1u << d))) continue;
-    for (int k = 0; k < per_dev; ++k) {
-      ctx->workers.emplace_back();
-      if (int rc = worker_init(ctx->workers.back(), d, (int)ctx->workers.size() - 1)) {
-        std::string msg = lbf_last_error();
-        lbf_ctx_destroy(ctx);
-        return fail(rc, msg);
+  lbf_ctx* ctx = new (std::nothrow) lbf_ctx();
+  if (!ctx) return fail(LBF_ERR_NOMEM, "host allocation failed");
+  const int rc = guarded([&] {
+    ctx->workers.reserve((size_t)std::min(ndev, 32) * (size_t)per_dev);  // workers never move once initialised
+    for (int d = 0; d < ndev && d < 32; ++d) {
+      if (device_mask && !(device_mask & (1u << d))) continue;
+      for (int k = 0; k < per_dev; ++k) {
+        ctx->workers.emplace_back();
+        if (int r = worker_init(ctx->workers.back(), d, (int)ctx->workers.size() - 1)) return r;
       }
     }
+    return (int)LBF_OK;
+  });
+  if (rc) {
+    std::string msg = lbf_last_error();
+    lbf_ctx_destroy(ctx);
+    return fail(rc, msg);
   }
   if (ctx->workers.empty()) {
     delete ctx;
@@ -1045,7 +1096,7 @@ extern "C" int lbf_sha1_batch(lbf_ctx* ctx, const uint8_t* base, uint64_t base_l
   job.sizes = sizes;
   job.digests = out_digests;
   if (int rc = validate_memory_job(job, n)) return rc;
-  return run_job(ctx, job, n);
+  return guarded([&] { return run_job(ctx, job, n); });
 }
 
 extern "C" int lbf_verify_batch(lbf_ctx* ctx, const uint8_t* base, uint64_t base_len, const uint64_t* offsets,
@@ -1064,7 +1115,7 @@ extern "C" int lbf_verify_batch(lbf_ctx* ctx, const uint8_t* base, uint64_t base
   job.expected = expected;
   job.verdicts = verdicts;
   if (int rc = validate_memory_job(job, n)) return rc;
-  return run_job(ctx, job, n);
+  return guarded([&] { return run_job(ctx, job, n); });
 }
 
 extern "C" int lbf_files_ranges(lbf_ctx* ctx, const char* const* paths, uint32_t n_files, const uint32_t* file_of,
@@ -1104,7 +1155,7 @@ extern "C" int lbf_files_ranges(lbf_ctx* ctx, const char* const* paths, uint32_t
   job.expected = expected;
   if (expected) job.verdicts = out;
   else job.digests = out;
-  return run_job(ctx, job, n);
+  return guarded([&] { return run_job(ctx, job, n); });
 }
 
 extern "C" int lbf_file_ranges(lbf_ctx* ctx, const char* path, const uint64_t* offsets, const uint32_t* sizes,
