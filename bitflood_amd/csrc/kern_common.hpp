@@ -66,8 +66,18 @@ template <bool kUniform>
 __device__ __forceinline__ ChainInfo chain_info(const ChunkParams& p, uint32_t i) {
   ChainInfo c{};
   if (i >= p.n) {
-    c.src = p.base;
-    return c;
+    // A lane past the end of the table runs a copy of its wave's first chain
+    // (no result is ever written for it).  The producer waves then take one
+    // branch per step for the whole wave, instead of building a padding block
+    // for the idle lanes next to the live lanes' full blocks: a wave with
+    // idle lanes -- one chunk through Base64Encode, the last wave of a batch
+    // -- ran at ≈2,380 rather than ≈1,810 cycles per block.
+    const uint32_t first = i & ~63u;
+    if (first >= p.n) {
+      c.src = p.base;
+      return c;
+    }
+    i = first;
   }
   uint64_t off;
   if (kUniform) {

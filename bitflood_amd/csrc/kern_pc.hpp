@@ -198,7 +198,10 @@ __device__ __forceinline__ void p2_dma(const ChainInfo& c, uint32_t step, uint32
 }
 
 // The 16 message words of `step`: full blocks from the raw slot (aligned) or
-// global memory (misaligned), final blocks built from the tail.
+// global memory (misaligned), final blocks built from the tail.  Past its last
+// block a lane's words are never used: it only zeroes them, so a ragged wave
+// pays for the final-block branch only in the steps where some lane really
+// builds one.
 __device__ __forceinline__ void p2_block(uint32_t (&w)[16], const uint4* raw, const ChainInfo& c, uint32_t step) {
   if (step < c.nfull) {
     if (c.aligned) {
@@ -208,8 +211,11 @@ __device__ __forceinline__ void p2_block(uint32_t (&w)[16], const uint4* raw, co
 #pragma unroll
       for (int k = 0; k < 16; ++k) w[k] = bswap(w[k]);
     }
-  } else {
+  } else if (step < c.total) {
     final_block(w, c.src + 64ull * c.nfull, c.size & 63u, c.size, step != c.nfull);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) w[k] = 0;
   }
 }
 

@@ -305,6 +305,8 @@ __device__ __forceinline__ void px5_produce(uint4* ring, uint32_t raw_lds, const
 #pragma unroll
     for (int k = 0; k < 16; ++k) w[k] = bswap(w[k]);
   } else {
+    // (zeroing the words of lanes past their last block instead, as p2_block
+    // does, cost C4 0.6 %: profiles/r02/idle_lanes/)
     final_block(w, c.src + 64ull * c.nfull, c.size & 63u, c.size, step != c.nfull);
   }
   // The consumer reads words 0..15 of every step from the raw slot: the
