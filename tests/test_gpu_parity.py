@@ -80,6 +80,28 @@ def test_random_batch_vs_oracle(variant, hasher, oracle):
     assert bad.size == 0, f"{bad.size} mismatches, first at {bad[:5]} sizes {sizes[bad[:5]]}"
 
 
+@pytest.mark.parametrize("n", [1, 2, 63, 65, 127, 129])
+def test_partial_waves_hash_and_verify(variant, hasher, oracle, n):
+    """Waves with idle lanes (n not a multiple of 64): those lanes run a copy of
+    their wave's first chain and write nothing (kern_common.hpp chain_info).
+    The first chain of each wave is made the longest, or unaligned, so that a
+    copy that leaked into a result or outlived the real chains would show."""
+    rng = np.random.default_rng(1000 + n)
+    buf = oracle.synth(31, 0, 4 << 20)
+    sizes = rng.integers(0, 150000, n).astype(np.uint32)
+    offs = np.array([rng.integers(0, buf.size - s + 1) for s in sizes], dtype=np.uint64) & ~np.uint64(15)
+    for w0 in range(0, n, 64):
+        sizes[w0] = 200000 + w0
+        offs[w0] = 4096 * (w0 // 64) + (w0 // 64) % 2 * 5  # odd waves: first chain unaligned
+    want = oracle.sha1_batch(buf, offs, sizes)
+    got = hasher.hash_chunks(buf, offs, sizes)
+    assert np.array_equal(got, want)
+    exp = want.copy()
+    exp[-1, 7] ^= 0x10
+    v = hasher.verify_chunks(buf, offs, sizes, exp)
+    assert v[:-1].all() and not v[-1]
+
+
 def test_empty_inputs(variant, hasher):
     assert hasher.sha1(b"").hex() == "da39a3ee5e6b4b0d3255bfef95601890afd80709"
     out = hasher.hash_chunks(np.zeros(16, np.uint8), np.zeros(0, np.uint64), np.zeros(0, np.uint32))
