@@ -78,6 +78,8 @@ def parse():
                     help="0 = every CPU this process may use (affinity, capped by the cgroup CPU quota)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host->device->host rate")
+    ap.add_argument("--no-other-configs", action="store_true",
+                    help="skip the device-resident C3 and C4 measurements that follow the main line at N=1")
     a = ap.parse_args()
     a.chunk_size = a.chunk_size or {"c2": 262144, "c4": 1 << 20}[a.config]
     a.file_gib = a.file_gib or {"c2": 4.0, "c4": 32.0}[a.config]
@@ -298,6 +300,71 @@ def check_golden(gold, digests):
     return 1 if ok else 0
 
 
+def other_configs():
+    """C3 and C4 (BASELINE.json configs[2], configs[3] per GPU), device-resident,
+    measured after the main line at N=1 and checked against their goldens:
+    secondary numbers for DESIGN.md §5, never `value`.  A failure is recorded,
+    not raised."""
+    g = os.path.join(ROOT, "tests", "golden")
+    res = {}
+    stream = torch.cuda.current_stream()
+    sptr = stream.cuda_stream
+
+    def timed(buf, length, cs, n, dig, reps=3):
+        H.uniform_launch(buf, length, cs, 0, n, dig, stream=sptr)  # warm-up
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            H.uniform_launch(buf, length, cs, 0, n, dig, stream=sptr)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / reps
+
+    def entry(name, length, cs, ms, ok, gold):
+        return {"workload": name, "bytes": length, "chunk_size": cs, "chunks": length // cs,
+                "kernel": KERNELS.get(H.load().lbf_kernel_for(length // cs), "?"), "ms_per_launch": round(ms, 4),
+                "gibs": round(length / GIB / (ms / 1e3), 1),
+                "hbm_frac": round(length / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4), "golden": gold, "parity": ok}
+
+    for name in ("C3", "C4"):
+        buf = dig = None
+        try:
+            if name == "C3":
+                c3 = json.load(open(os.path.join(g, "c3.json")))
+                fs, cs = c3["file_size"], c3["chunk_size"]
+                length = fs * len(c3["files"])
+                buf = DeviceBuffer(length)
+                for f in range(len(c3["files"])):  # file f = stream seed f from byte 0
+                    buf.fill_synthetic(f, start=0, nbytes=fs, stream=sptr, offset=f * fs)
+                n = length // cs
+                dig = DeviceBuffer(n * 20)
+                ms = timed(buf, length, cs, n, dig)
+                d = dig.download(n * 20)
+                ok = hashlib.sha1(d.tobytes()).hexdigest() == c3["sha1_of_all_digests_in_file_order_hex"]
+                res[name] = entry("C3: 64 files x 1 GiB, 256 KiB chunks, one launch", length, cs, ms, ok,
+                                  "tests/golden/c3.json")
+            else:
+                c4 = json.load(open(os.path.join(g, "c4.json")))
+                cs, length = c4["chunk_size"], 32 * GIB
+                gold = next(r for r in c4["shards"] if r["rank"] == 0)
+                buf = DeviceBuffer(length)
+                buf.fill_synthetic(SEED_C, start=0, stream=sptr)
+                n = length // cs
+                dig = DeviceBuffer(n * 20)
+                ms = timed(buf, length, cs, n, dig)
+                ok = check_golden(gold, dig.download(n * 20).reshape(n, 20)) == 1
+                res[name] = entry("C4 per GPU: shard 0 (32 GiB) of the 256 GiB file, 1 MiB chunks", length, cs, ms,
+                                  ok, "tests/golden/c4.json shard 0")
+        except Exception as e:  # recorded in the line; the main measurement stands
+            res[name] = {"error": f"{type(e).__name__}: {e}"}
+        finally:
+            for b in (buf, dig):
+                if b is not None:
+                    b.free()
+    return res
+
+
 def gather_ints(x, world):
     if world == 1:
         return [int(x)]
@@ -448,6 +515,8 @@ def main():
         out["first_chunk_b64"] = b64_27(bytes(digests[0]))
     buf.free()
     dig.free()
+    if rank == 0 and world == 1 and not args.no_other_configs and args.config == "c2":
+        out["other_configs"] = other_configs()
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
