@@ -945,6 +945,8 @@ int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
     rc = fail(LBF_ERR_NOMEM, "host allocation failed while staging");
   } catch (const std::system_error& e) {
     rc = fail(LBF_ERR_NOMEM, std::string("host resources while staging: ") + e.what());
+  } catch (const std::exception& e) {
+    rc = fail(LBF_ERR_INVALID, std::string("internal error while staging: ") + e.what());
   }
   // drain, on every path (every H2D ran on a device slot's stream, so this also
   // completes every host slot's copy)
