@@ -359,6 +359,7 @@ struct Worker {
   uint64_t desc_cap = 0;    // descriptors per group
   uint64_t hdr_cap = 0;     // header_bytes(desc_cap)
   long fault_group = -1;    // LBF_TEST_FAULT_GROUP (tests only, one shot)
+  bool fault_throws = false;  // LBF_TEST_FAULT_KIND=throw: the fault is a host exception, not a HIP error
 };
 
 }  // namespace
@@ -499,6 +500,8 @@ int worker_init(Worker& w, int device, int index) {
   // Test hook: fail the g-th group this worker stages (once), after earlier
   // groups are in flight, to exercise the drain on the error path.
   if (env_long("LBF_TEST_FAULT_WORKER", 0) == index) w.fault_group = env_long("LBF_TEST_FAULT_GROUP", -1);
+  const char* kind = getenv("LBF_TEST_FAULT_KIND");
+  w.fault_throws = kind && strcmp(kind, "throw") == 0;
   LBF_HIP_TRY(hipSetDevice(device));
   if (numa_enabled()) {
     w.numa_node = device_numa_node(device);
@@ -846,6 +849,7 @@ int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
       if ((rc = finalize(job, order, s))) break;
       if (group++ == w.fault_group) {
         w.fault_group = -1;
+        if (w.fault_throws) throw std::bad_alloc();  // must still reach the drain
         rc = fail(LBF_ERR_HIP, "injected fault (LBF_TEST_FAULT_GROUP) at group " + std::to_string(group - 1));
         break;
       }

@@ -94,21 +94,26 @@ def test_multi_worker_file_paths(workers, oracle, monkeypatch, tmp_path):
         h.close()
 
 
+@pytest.mark.parametrize("kind", ["hip", "throw"])
 @pytest.mark.parametrize("workers,fault_worker", [(1, 0), (4, 3)])
-def test_injected_fault_drains_before_next_job(workers, fault_worker, oracle, monkeypatch):
-    """A HIP-side failure in the middle of a job (LBF_TEST_FAULT_GROUP: the
-    worker's third staging group fails after two are in flight) returns
-    LBF_ERR_HIP; every slot is drained, so the next, smaller job on the same
-    context gets exactly its own results (a stale pending group
-    used to be finalized into the next job's arrays)."""
+def test_injected_fault_drains_before_next_job(workers, fault_worker, kind, oracle, monkeypatch):
+    """A failure in the middle of a job (LBF_TEST_FAULT_GROUP: the worker's
+    third staging group fails after two are in flight) returns LBF_ERR_HIP for
+    a HIP-side error, LBF_ERR_NOMEM for a host exception (which must not cross
+    the C ABI); every slot is drained either way, so the next, smaller job on
+    the same context gets exactly its own results (a stale pending
+    group used to be finalized into the next job's arrays)."""
     h = _ctx(monkeypatch, LBF_WORKERS_PER_DEVICE=workers, LBF_SLOT_MB=8, LBF_TEST_FAULT_GROUP=2,
-             LBF_TEST_FAULT_WORKER=fault_worker)
+             LBF_TEST_FAULT_WORKER=fault_worker, LBF_TEST_FAULT_KIND=kind)
     try:
         big = oracle.synth(63, 0, 96 << 20, nthreads=8)
         offs, sizes = chunk_table(big.size, 65536)
         with pytest.raises(LbfError) as ei:
             h.hash_chunks(big, offs, sizes)
-        assert ei.value.status == _capi.LBF_ERR_HIP and "injected fault" in str(ei.value)
+        if kind == "hip":
+            assert ei.value.status == _capi.LBF_ERR_HIP and "injected fault" in str(ei.value)
+        else:
+            assert ei.value.status == _capi.LBF_ERR_NOMEM and "host allocation failed while staging" in str(ei.value)
         if workers > 1:
             assert f"worker {fault_worker} " in str(ei.value)
         small = oracle.synth(64, 0, (3 << 20) + 99)
