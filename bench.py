@@ -267,9 +267,11 @@ def e2e_rate(host_data, cs):
         # warm: one untimed pass sizes the context's pinned staging to this job
         # (it grows on demand; tools/file_rate.py reports the one-shot cost)
         h.hash_chunks(host_data, offs, sizes)
-        t0 = time.perf_counter()
-        d = h.hash_chunks(host_data, offs, sizes)
-        t = time.perf_counter() - t0
+        t = float("inf")
+        for _ in range(3):  # best of 3: a lone pass swings with the host's other tenants
+            t0 = time.perf_counter()
+            d = h.hash_chunks(host_data, offs, sizes)
+            t = min(t, time.perf_counter() - t0)
         placement = h.worker_info(0)
     return host_data.size / GIB / t, d, placement
 
