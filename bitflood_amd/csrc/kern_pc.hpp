@@ -402,8 +402,11 @@ __device__ __forceinline__ void pc4_compress(Digest& s, const uint4 (&cur)[kPcQu
 // profiles/r01/probe_lds_lanes.log).  The lgkm counter holds 15, so the next
 // step's 40 pairs go out in three batches: before round 0, after round 16 and
 // after round 40, each pinned by fences like the late loads of pc4_compress.
+// Even batch sizes (14, 14, 12) let the compiler pair every load into a
+// ds_read2st64_b64: 20 LDS instructions per step instead of 21 with (15, 13,
+// 12) -- 0.1 %, inside the noise (profiles/r02/pc4_even_batches/).
 constexpr int kPc5Pairs = 40;
-constexpr int kPc5B1 = 15, kPc5B1At = 7;   // pairs 0..14 first; 15..27 after pair 7's rounds
+constexpr int kPc5B1 = 14, kPc5B1At = 7;   // pairs 0..13 first; 14..27 after pair 7's rounds
 constexpr int kPc5B2 = 28, kPc5B2At = 19;  // pairs 28..39 after pair 19's rounds
 // kSplit keeps every load a single ds_read_b64: a memory fence between loads
 // stops the compiler from pairing them into ds_read2st64_b64 (which returns
