@@ -265,6 +265,8 @@ __device__ __forceinline__ void px5_compress(Digest& s, const Px5Sched& cur, Px5
       const int hi = q == kPx5B1At ? kPx5B2 : 32;
 #pragma unroll
       for (int r = lo; r < hi; ++r) nxt.v[r] = next_pairs[r * kPcLanes];
+      // (all five operands: fencing on e alone, as pc5_compress does, dropped the
+      // s_nop after it but cost C4 1.1 %, profiles/r02/pc4_light_fence/c4/)
       asm volatile("" : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+v"(e)::"memory");
     }
   }
