@@ -596,8 +596,11 @@ __global__ void __launch_bounds__(192) sha1_pc4_kernel(ChunkParams p) {
     uint32_t k = 0;
     // Four steps per iteration while every chain of the workgroup is running
     // and every step is followed by a barrier: k % 4 == 0, so the slots are
-    // compile-time offsets and the steps need no liveness checks.
-    for (; k + 4 <= min_steps && k + 4 < nsteps; k += 4) {
+    // compile-time offsets and the steps need no liveness checks.  The two
+    // conditions are folded into one bound, so the loop test is one scalar
+    // compare (the compiler built the conjunction from 7 scalar ops).
+    const uint32_t fast_end = __builtin_amdgcn_readfirstlane(nsteps ? min(min_steps, nsteps - 1) : 0u);
+    for (; k + 4 <= fast_end; k += 4) {
       pc4_step(s, A, B, Pc4Sched<kVec>::col(ring, 1, lane), true, true);
       pc4_barrier(s PC4_ACC);  // barrier k+1
       pc4_step(s, B, A, Pc4Sched<kVec>::col(ring, 2, lane), true, true);
