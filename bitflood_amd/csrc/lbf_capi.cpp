@@ -213,6 +213,19 @@ constexpr int kMpolDefault = 0, kMpolPreferred = 1;
 constexpr unsigned long kMpolFNode = 1, kMpolFAddr = 2;
 constexpr unsigned long kMaxNodes = 1024;
 
+// The caller's current HIP device is its own state (a torch process keeps its
+// tensors on it): entry points that switch devices to create, drive or free
+// workers put it back on the way out.
+struct KeepCurrentDevice {
+  int saved = -1;
+  KeepCurrentDevice() {
+    if (hipGetDevice(&saved) != hipSuccess) saved = -1;
+  }
+  ~KeepCurrentDevice() {
+    if (saved >= 0) (void)hipSetDevice(saved);
+  }
+};
+
 bool numa_enabled() {
   static const bool on = env_long("LBF_NUMA", 1) != 0;
   return on;
@@ -978,6 +991,7 @@ int validate_memory_job(const Job& job, uint64_t n) {
 // worker's NUMA node), no collective.
 int run_job(lbf_ctx* ctx, const Job& job, uint64_t n) {
   std::lock_guard<std::mutex> lock(ctx->mu);
+  KeepCurrentDevice keep;  // worker 0 (and any inline worker) runs on this thread
   const size_t nw = ctx->workers.size();
   if (nw == 1 || n < 2 * nw) return worker_run(ctx->workers[0], job, 0, n);
   std::vector<int> rcs(nw, LBF_OK);
@@ -1009,6 +1023,7 @@ int run_job(lbf_ctx* ctx, const Job& job, uint64_t n) {
 int run_device_job(lbf_ctx* ctx, const uint8_t* base, const uint64_t* offsets, const uint32_t* sizes,
                    uint64_t n, uint8_t* digests, const uint8_t* expected, uint8_t* verdicts) {
   std::lock_guard<std::mutex> lock(ctx->mu);
+  KeepCurrentDevice keep;
   Worker& w = ctx->workers[0];
   LBF_HIP_TRY(hipSetDevice(w.device));
   hipStream_t s = w.dev[0].stream;
@@ -1034,6 +1049,7 @@ extern "C" int lbf_ctx_create(uint32_t device_mask, lbf_ctx** out) {
   // per-worker staging and the error propagation of run_job run on a one-GPU
   // box exactly as they do with one worker per GPU on an 8-GPU node.
   const int per_dev = (int)std::max(1L, std::min(16L, env_long("LBF_WORKERS_PER_DEVICE", 1)));
+  KeepCurrentDevice keep;  // worker_init selects each worker's device
   lbf_ctx* ctx = new (std::nothrow) lbf_ctx();
   if (!ctx) return fail(LBF_ERR_NOMEM, "host allocation failed");
   const int rc = guarded([&] {
@@ -1075,6 +1091,7 @@ extern "C" int lbf_ctx_worker_info(const lbf_ctx* ctx, int worker, int* device, 
 
 extern "C" void lbf_ctx_destroy(lbf_ctx* ctx) {
   if (!ctx) return;
+  KeepCurrentDevice keep;
   for (Worker& w : ctx->workers) worker_free(w);
   delete ctx;
 }

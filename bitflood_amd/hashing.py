@@ -233,12 +233,20 @@ class DeviceBuffer:
             check(load().lbf_dev_free(self.ptr))
             self.ptr = None
 
+    def _range(self, offset: int, nbytes: int, what: str):
+        if not self.ptr:
+            raise ValueError(f"{what}: buffer already freed")
+        if offset < 0 or nbytes < 0 or offset + nbytes > self.nbytes:
+            raise ValueError(f"{what}: [{offset}, {offset + nbytes}) outside the {self.nbytes}-byte buffer")
+
     def upload(self, host: np.ndarray, offset: int = 0):
         host = np.ascontiguousarray(host)
+        self._range(offset, host.nbytes, "upload")
         check(load().lbf_memcpy_h2d(self.ptr + offset, host.ctypes.data, host.nbytes))
 
     def download(self, nbytes: int | None = None, offset: int = 0, dtype=np.uint8) -> np.ndarray:
         nbytes = self.nbytes - offset if nbytes is None else nbytes
+        self._range(offset, nbytes, "download")
         out = np.empty(nbytes, dtype=np.uint8)
         check(load().lbf_memcpy_d2h(out.ctypes.data, self.ptr + offset, nbytes))
         return out.view(dtype)
@@ -247,8 +255,7 @@ class DeviceBuffer:
         """Bytes [start, start+nbytes) of synthetic stream `seed` into this
         buffer at byte `offset` (16-byte aligned)."""
         nbytes = self.nbytes - offset if nbytes is None else nbytes
-        if offset < 0 or offset + nbytes > self.nbytes:
-            raise ValueError("fill_synthetic: range outside the buffer")
+        self._range(offset, nbytes, "fill_synthetic")
         check(load().lbf_fill_synthetic(self.ptr + offset, nbytes, seed, start, stream))
 
 

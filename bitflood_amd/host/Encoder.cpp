@@ -9,6 +9,7 @@
 
 #include <sys/stat.h>
 
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -21,7 +22,9 @@ namespace Encoder {
 namespace {
 
 std::mutex g_mu;
-lbf_ctx* g_ctx = nullptr;
+// Shared: SetDeviceMask drops the process's reference, and calls still running
+// on other threads keep theirs until they return.
+std::shared_ptr<lbf_ctx> g_ctx;
 U32 g_mask = 0;
 thread_local std::string t_err;
 
@@ -40,35 +43,39 @@ std::string b64(const U8* digest) {
 struct CtxReaper {
   ~CtxReaper() {
     std::lock_guard<std::mutex> lock(g_mu);
-    if (g_ctx) lbf_ctx_destroy(g_ctx);
-    g_ctx = nullptr;
+    g_ctx.reset();
   }
 } g_reaper;
 
 }  // namespace
 
-lbf_ctx* Context() {
+std::shared_ptr<lbf_ctx> SharedContext() {
   std::lock_guard<std::mutex> lock(g_mu);
   if (!g_ctx) {
     lbf_ctx* c = nullptr;
-    if (lbf_ctx_create(g_mask, &c) == LBF_OK) g_ctx = c;
+    if (lbf_ctx_create(g_mask, &c) == LBF_OK) g_ctx.reset(c, lbf_ctx_destroy);
     else fail("lbf_ctx_create");
   }
   return g_ctx;
 }
 
+lbf_ctx* Context() { return SharedContext().get(); }
+
 Error::ErrorCode SetDeviceMask(U32 i_mask) {
-  std::lock_guard<std::mutex> lock(g_mu);
-  if (g_ctx) lbf_ctx_destroy(g_ctx);
-  g_ctx = nullptr;
-  g_mask = i_mask;
-  return Error::NO_ERROR_LBF;
+  std::shared_ptr<lbf_ctx> old;
+  {
+    std::lock_guard<std::mutex> lock(g_mu);
+    old.swap(g_ctx);
+    g_mask = i_mask;
+  }
+  return Error::NO_ERROR_LBF;  // `old` is destroyed here unless a call still holds it
 }
 
 const char* LastError() { return t_err.c_str(); }
 
 Error::ErrorCode Base64Encode(const U8* i_data, U32 i_size, std::string& o_string) {
-  lbf_ctx* ctx = Context();
+  const std::shared_ptr<lbf_ctx> held = SharedContext();  // alive for the whole call
+  lbf_ctx* ctx = held.get();
   if (!ctx) return Error::UNKNOWN_ERROR_LBF;
   U8 d[20];
   if (lbf_sha1_one(ctx, i_data, i_size, d) != LBF_OK) return fail("Base64Encode");
@@ -80,7 +87,8 @@ Error::ErrorCode HashChunks(const U8* i_base, U64 i_len, const U64* i_offsets, c
                             V_U8& o_digests) {
   o_digests.assign(i_n * 20, 0);
   if (i_n == 0) return Error::NO_ERROR_LBF;
-  lbf_ctx* ctx = Context();
+  const std::shared_ptr<lbf_ctx> held = SharedContext();  // alive for the whole call
+  lbf_ctx* ctx = held.get();
   if (!ctx) return Error::UNKNOWN_ERROR_LBF;
   if (lbf_sha1_batch(ctx, i_base, i_len, i_offsets, i_sizes, i_n, o_digests.data(), LBF_HOST_PTR) != LBF_OK)
     return fail("HashChunks");
@@ -109,7 +117,8 @@ Error::ErrorCode EncodeFile(const ToEncode& i_toencode, FloodFile& o_floodfile) 
     t_err = "EncodeFile: empty file list or zero chunk size";
     ret = Error::UNKNOWN_ERROR_LBF;
   } else {
-    lbf_ctx* ctx = Context();
+    const std::shared_ptr<lbf_ctx> held = SharedContext();  // alive for the whole call
+    lbf_ctx* ctx = held.get();
     if (!ctx) return Error::UNKNOWN_ERROR_LBF;
     const U64 cs = i_toencode.m_chunksize;
     std::vector<const char*> paths;  // files that exist, in the given order

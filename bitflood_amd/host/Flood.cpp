@@ -10,6 +10,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <map>
+#include <memory>
+#include <system_error>
 #include <thread>
 #include <vector>
 
@@ -37,11 +39,20 @@ void parallel_for(size_t n, unsigned threads, F f) {
     return;
   }
   std::atomic<size_t> next{0};
+  auto pull = [&] {
+    for (size_t k; (k = next++) < n;) f(k);
+  };
+  // helpers plus the calling thread; a helper that cannot be started leaves
+  // its share to the others (a joinable thread must never be destroyed)
   std::vector<std::thread> th;
-  for (unsigned t = 0; t < threads; ++t)
-    th.emplace_back([&] {
-      for (size_t k; (k = next++) < n;) f(k);
-    });
+  for (unsigned t = 1; t < threads; ++t) {
+    try {
+      th.emplace_back(pull);
+    } catch (const std::system_error&) {
+      break;
+    }
+  }
+  pull();
   for (auto& t : th) t.join();
 }
 
@@ -53,7 +64,10 @@ unsigned io_threads() {
 
 }  // namespace
 
-lbf_ctx* Flood::Ctx() const { return m_ctx ? m_ctx : Encoder::Context(); }
+std::shared_ptr<lbf_ctx> Flood::Ctx() const {
+  if (m_ctx) return std::shared_ptr<lbf_ctx>(m_ctx, [](lbf_ctx*) {});  // the caller owns it
+  return Encoder::SharedContext();
+}
 
 std::string Flood::PathOf(const std::string& i_name) const {
   if (m_rootdir.empty() || (!i_name.empty() && i_name[0] == '/')) return i_name;
@@ -74,7 +88,8 @@ Error::ErrorCode Flood::SetupFilesAndChunks() {
   m_runtimefiles.clear();
   m_chunkstodownload.clear();
   if (!m_floodfile) return Error::UNKNOWN_ERROR_LBF;
-  lbf_ctx* ctx = Ctx();
+  const std::shared_ptr<lbf_ctx> held = Ctx();  // alive for the whole call
+  lbf_ctx* ctx = held.get();
   if (!ctx) return Error::UNKNOWN_ERROR_LBF;
   Error::ErrorCode ret = Error::NO_ERROR_LBF;
   std::vector<RuntimeFile> rtfs;
@@ -171,7 +186,8 @@ Error::ErrorCode Flood::ReadVerifiedChunk(const std::string& i_filename, U32 i_c
     o_data.clear();
     return Error::NO_ERROR_LBF;
   }
-  lbf_ctx* ctx = Ctx();
+  const std::shared_ptr<lbf_ctx> held = Ctx();  // alive for the whole call
+  lbf_ctx* ctx = held.get();
   if (!ctx) return Error::UNKNOWN_ERROR_LBF;
   const U64 zero = 0;
   const U32 sz = chunk.m_size;
@@ -199,7 +215,8 @@ Error::ErrorCode Flood::ReceiveChunk(const std::string& i_filename, U32 i_chunki
   if (chunk.m_size != i_size) return Error::NO_ERROR_LBF;  // :156
   U8 expected[20];
   if (!decode_hash(chunk.m_hash, expected)) return Error::NO_ERROR_LBF;
-  lbf_ctx* ctx = Ctx();
+  const std::shared_ptr<lbf_ctx> held = Ctx();  // alive for the whole call
+  lbf_ctx* ctx = held.get();
   if (!ctx) return Error::UNKNOWN_ERROR_LBF;
   const U64 zero = 0;
   U8 verdict = 0;
@@ -272,7 +289,8 @@ Error::ErrorCode Flood::ReadVerifiedChunks(const std::vector<P_ChunkKey>& i_keys
     vexp.insert(vexp.end(), &expected[20 * k], &expected[20 * k] + 20);
   }
   if (which.empty()) return Error::NO_ERROR_LBF;
-  lbf_ctx* ctx = Ctx();
+  const std::shared_ptr<lbf_ctx> held = Ctx();  // alive for the whole call
+  lbf_ctx* ctx = held.get();
   if (!ctx) return Error::UNKNOWN_ERROR_LBF;
   std::vector<U8> verdict(which.size(), 0);
   if (lbf_verify_batch(ctx, &o_arena[0], o_arena.size(), &voff[0], &vsz[0], which.size(), &vexp[0], &verdict[0],
@@ -306,7 +324,8 @@ Error::ErrorCode Flood::VerifyChunks(const U8* i_arena, U64 i_arena_len, const s
     vexp.insert(vexp.end(), e, e + 20);
   }
   if (which.empty()) return Error::NO_ERROR_LBF;
-  lbf_ctx* ctx = Ctx();
+  const std::shared_ptr<lbf_ctx> held = Ctx();  // alive for the whole call
+  lbf_ctx* ctx = held.get();
   if (!ctx) return Error::UNKNOWN_ERROR_LBF;
   std::vector<U8> verdict(which.size(), 0);
   static const U8 kEmpty = 0;

@@ -4,6 +4,8 @@
 // paths of Flood (ChunkMethods.cpp:89-225 restated) on a real file.
 //   lbf_gpu_tests <scratch-dir>
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -99,6 +101,28 @@ int main(int argc, char** argv) {
       });
     for (auto& x : th) x.join();
     for (int t = 0; t < 8; ++t) CHECK(bad[t] == 0);
+
+    // SetDeviceMask replaces the process context while other threads hash:
+    // their calls keep the context they started with (shared ownership), so
+    // every result is still exact and nothing runs on a destroyed context.
+    std::atomic<bool> stop{false};
+    std::vector<int> bad2(4, 0);
+    std::vector<std::thread> th2;
+    for (int t = 0; t < 4; ++t)
+      th2.emplace_back([&, t] {
+        for (U32 k = (U32)t; !stop; k = (k + 4) % 64) {
+          std::string s2;
+          if (Encoder::Base64Encode(buf.data() + at[k], len[k], s2) != Error::NO_ERROR_LBF || s2 != one[k]) ++bad2[t];
+        }
+      });
+    for (int sw = 0; sw < 20; ++sw) {
+      CHECK(Encoder::SetDeviceMask(sw & 1 ? 1u : 0u) == Error::NO_ERROR_LBF);
+      std::this_thread::sleep_for(std::chrono::milliseconds(20));
+    }
+    stop = true;
+    for (auto& x : th2) x.join();
+    for (int t = 0; t < 4; ++t) CHECK(bad2[t] == 0);
+    CHECK(Encoder::SetDeviceMask(0) == Error::NO_ERROR_LBF);
   }
 
   // EncodeFile -> Flood: seeder read-verify, receiver accept/reject
