@@ -25,6 +25,8 @@
 #include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
+#include <iterator>
+#include <map>
 #include <mutex>
 #include <new>
 #include <stdexcept>
@@ -50,6 +52,10 @@ int fail(int status, const std::string& msg) {
 }
 
 int hip_fail(hipError_t e, const char* what) {
+  // HIP keeps a failed call's status as the thread's last error; left there,
+  // it surfaces from the hipGetLastError() after the NEXT kernel launch and
+  // fails a call that did nothing wrong.  The status is reported here instead.
+  (void)hipGetLastError();
   return fail(e == hipErrorOutOfMemory ? LBF_ERR_NOMEM : LBF_ERR_HIP,
               std::string(what) + ": " + hipGetErrorString(e));
 }
@@ -371,14 +377,27 @@ struct Worker {
   uint64_t dev_budget = 0;  // LBF_DEVICE_STAGING_MB: HBM for device slots
   uint64_t desc_cap = 0;    // descriptors per group
   uint64_t hdr_cap = 0;     // header_bytes(desc_cap)
+  uint64_t bytes_staged = 0;  // chunk bytes sent through the pinned ring (cumulative)
+  uint64_t bytes_direct = 0;  // chunk bytes sent straight from registered caller memory
   long fault_group = -1;    // LBF_TEST_FAULT_GROUP (tests only, one shot)
   bool fault_throws = false;  // LBF_TEST_FAULT_KIND=throw: the fault is a host exception, not a HIP error
 };
 
 }  // namespace
 
+namespace {
+// Caller memory registered with lbf_host_register: [lo, hi) page-rounded, as
+// pinned; `owned` = this context registered it (and unregisters it).
+struct Registered {
+  uintptr_t user = 0;  // the pointer the caller passed (the unregister key)
+  uintptr_t lo = 0, hi = 0;
+  bool owned = false;
+};
+}  // namespace
+
 struct lbf_ctx {
   std::vector<Worker> workers;
+  std::vector<Registered> regs;  // guarded by mu, like every job
   std::mutex mu;
 };
 
@@ -553,6 +572,7 @@ struct Source {
   const uint8_t* base = nullptr;  // memory source
   uint64_t base_len = 0;
   std::vector<int> fds;           // file source: one fd per file, -1 = could not be opened
+  bool pinned = false;            // [base, base+base_len) lies in a lbf_host_register'ed range
   unsigned threads = copy_threads();  // staging copy threads
 
   bool from_files() const { return !fds.empty(); }
@@ -734,6 +754,18 @@ int run_oversize(Worker& w, const Job& job, uint64_t i) {
 // is copied along (cheaper than another copy); the 16-byte padding between
 // ReadVerifiedChunks' arena slots is the common case.
 constexpr uint64_t kJoinGap = 4096;
+// A registered (pinned) source goes to the device without the staging copy,
+// one H2D per run, when its group's runs average at least kDirectMinRun:
+// below that, per-copy overhead costs more than the host memcpy it saves.
+// And only for a worker's job of at most kDirectMaxJob bytes.  Measured on
+// one MI355X (tools/e2e_sizes.py --register): direct is 15 %
+// faster at 64-256 MiB (no host copy ahead of the first H2D) but 14-15 %
+// slower at 1-4 GiB, because there a group's H2D from registered memory did
+// not start before the previous group's kernel had finished (rocprofv3 trace,
+// profiles/r02/registered_trace/), while the staged pieces overlap the
+// kernels.
+constexpr uint64_t kDirectMinRun = 1ull << 20;
+constexpr uint64_t kDirectMaxJob = 512ull << 20;
 
 // Process descriptors [begin, end) on one worker.  They are staged in source
 // order: sorted by offset (a stable permutation, skipped when the table is
@@ -767,6 +799,7 @@ int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
       std::stable_sort(order.perm.begin(), order.perm.end(), before);
       break;
     }
+  uint64_t job_bytes = 0;  // the union of this worker's runs
   {
     // Staging sized to the bytes this worker stages (the union of its runs):
     // a quarter of them per slot once they exceed kSplitMin, so a mid-sized job
@@ -789,6 +822,7 @@ int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
         open = true;
       }
     }
+    job_bytes = bytes;
     uint64_t per = bytes <= kSplitMin ? bytes : std::max({kSplitMin, (bytes + 3) / 4, largest});
     per = std::min(per, w.slot_max);
     // Long chains: a batch's kernel lasts one chain (≈1 µs per 64-byte block)
@@ -806,6 +840,7 @@ int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
       if (int rc = ensure_dev_slots(w, largest, groups)) return rc;
     }
   }
+  const bool direct_job = job.src.pinned && job_bytes <= kDirectMaxJob;
   int cur = 0, hcur = 0;
   uint64_t i = begin;
   int rc = LBF_OK;
@@ -873,13 +908,26 @@ int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
       // pieces of pin_bytes followed by the header from the slot's own pinned
       // header buffer.  A run cut by a piece boundary is read in parts; once a
       // part comes back short (EOF), the rest of that run is unavailable.
-      const bool single = hdr + cursor <= w.pin_bytes;
+      // A registered source skips the ring: each run is copied to the device
+      // straight from the caller's pinned memory, then the header follows.
+      const bool direct = direct_job && !runs.empty() && cursor >= runs.size() * kDirectMinRun;
+      const bool single = !direct && hdr + cursor <= w.pin_bytes;
       const uint64_t data_off = single ? hdr : w.hdr_cap;
       uint8_t* h_header = nullptr;
       for (Run& r : runs) r.avail = 0;
+      if (direct) {
+        for (Run& r : runs) {
+          if (!hip_ok(hipMemcpyAsync(s.d_buf + data_off + r.dst, job.src.base + r.src, r.len, hipMemcpyHostToDevice,
+                                     s.stream),
+                      "hipMemcpyAsync(H2D, registered source)"))
+            break;
+          r.avail = r.len;
+        }
+      }
+      (direct ? w.bytes_direct : w.bytes_staged) += cursor;
       std::vector<bool> cut_short(runs.size(), false);
       size_t first_run = 0;
-      for (uint64_t pstart = 0; (pstart < cursor || (single && pstart == 0)) && rc == LBF_OK;) {
+      for (uint64_t pstart = 0; !direct && (pstart < cursor || (single && pstart == 0)) && rc == LBF_OK;) {
         const uint64_t room = single ? cursor : w.pin_bytes;
         const uint64_t pend = std::min(cursor, pstart + room);
         HostSlot& h = w.host[hcur];
@@ -989,9 +1037,17 @@ int validate_memory_job(const Job& job, uint64_t n) {
 
 // Contiguous index ranges per worker, one host thread each (bound to its
 // worker's NUMA node), no collective.
-int run_job(lbf_ctx* ctx, const Job& job, uint64_t n) {
+bool in_registered(const lbf_ctx* ctx, const uint8_t* base, uint64_t len) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(base);
+  for (const Registered& r : ctx->regs)
+    if (a >= r.lo && a <= r.hi && len <= r.hi - a) return true;
+  return false;
+}
+
+int run_job(lbf_ctx* ctx, Job job, uint64_t n) {
   std::lock_guard<std::mutex> lock(ctx->mu);
   KeepCurrentDevice keep;  // worker 0 (and any inline worker) runs on this thread
+  if (!job.src.from_files()) job.src.pinned = in_registered(ctx, job.src.base, job.src.base_len);
   const size_t nw = ctx->workers.size();
   if (nw == 1 || n < 2 * nw) return worker_run(ctx->workers[0], job, 0, n);
   std::vector<int> rcs(nw, LBF_OK);
@@ -1037,6 +1093,35 @@ int run_device_job(lbf_ctx* ctx, const uint8_t* base, const uint64_t* offsets, c
   return LBF_OK;
 }
 
+}  // namespace
+
+// Caller-pinned sources (lbf_host_register).  hipHostRegister pins whole
+// pages, portably (every device can DMA from them).  HIP does not count
+// registrations per caller: when a second context registered and then
+// unregistered a range the first one held, the first one's pin was gone
+// (its hipHostUnregister then failed; tests/test_gpu_registered.py, first
+// run).  So the library keeps one process-wide pin table: contexts
+// registering the same range share one pin (reference-counted), and memory
+// that something else already pinned (a hipHostMalloc'd buffer, a caller's
+// own hipHostRegister) is used as it is and never unpinned here.
+namespace {
+struct Pin {
+  uintptr_t hi = 0;
+  uint64_t refs = 0;
+};
+std::mutex g_pin_mu;
+std::map<uintptr_t, Pin> g_pins;  // lo -> pin, disjoint ranges
+
+// Drop one reference to the pin at lo (pinned by this library).
+int unpin(uintptr_t lo) {
+  std::lock_guard<std::mutex> lock(g_pin_mu);
+  auto it = g_pins.find(lo);
+  if (it == g_pins.end()) return LBF_OK;
+  if (--it->second.refs) return LBF_OK;
+  g_pins.erase(it);
+  LBF_HIP_TRY(hipHostUnregister(reinterpret_cast<void*>(lo)));
+  return LBF_OK;
+}
 }  // namespace
 
 extern "C" int lbf_ctx_create(uint32_t device_mask, lbf_ctx** out) {
@@ -1093,6 +1178,8 @@ extern "C" void lbf_ctx_destroy(lbf_ctx* ctx) {
   if (!ctx) return;
   KeepCurrentDevice keep;
   for (Worker& w : ctx->workers) worker_free(w);
+  for (const Registered& r : ctx->regs)
+    if (r.owned) (void)unpin(r.lo);  // teardown: nowhere to report a failure
   delete ctx;
 }
 
@@ -1104,6 +1191,79 @@ extern "C" int lbf_ctx_num_devices(const lbf_ctx* ctx) {
 }
 
 extern "C" int lbf_ctx_num_workers(const lbf_ctx* ctx) { return ctx ? (int)ctx->workers.size() : 0; }
+
+extern "C" int lbf_ctx_staging_stats(lbf_ctx* ctx, uint64_t* staged_bytes, uint64_t* direct_bytes) {
+  if (!ctx) return fail(LBF_ERR_INVALID, "null context");
+  std::lock_guard<std::mutex> lock(ctx->mu);  // between jobs
+  uint64_t st = 0, di = 0;
+  for (const Worker& w : ctx->workers) st += w.bytes_staged, di += w.bytes_direct;
+  if (staged_bytes) *staged_bytes = st;
+  if (direct_bytes) *direct_bytes = di;
+  return LBF_OK;
+}
+
+// Caller-pinned sources: see the pin table above lbf_ctx_create.
+extern "C" int lbf_host_register(lbf_ctx* ctx, const void* ptr, uint64_t len) {
+  if (!ctx || !ptr || len == 0) return fail(LBF_ERR_INVALID, "lbf_host_register: null context/pointer or empty range");
+  const uintptr_t page = (uintptr_t)sysconf(_SC_PAGESIZE);
+  const uintptr_t a = reinterpret_cast<uintptr_t>(ptr);
+  if (len > UINTPTR_MAX - a - page) return fail(LBF_ERR_INVALID, "lbf_host_register: range wraps");
+  Registered r;
+  r.user = a;
+  r.lo = a & ~(page - 1);
+  r.hi = (a + len + page - 1) & ~(page - 1);
+  return guarded([&] {
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    for (const Registered& o : ctx->regs)
+      if (r.lo < o.hi && o.lo < r.hi)
+        return fail(LBF_ERR_INVALID, "lbf_host_register: range overlaps one this context already holds");
+    ctx->regs.reserve(ctx->regs.size() + 1);  // nothing below may throw once pinned
+    std::lock_guard<std::mutex> pins(g_pin_mu);
+    auto next = g_pins.lower_bound(r.lo);
+    if (next != g_pins.end() && next->first == r.lo && next->second.hi == r.hi) {
+      ++next->second.refs;  // the same range, pinned by another context
+      r.owned = true;
+      ctx->regs.push_back(r);
+      return (int)LBF_OK;
+    }
+    const bool overlaps = (next != g_pins.end() && next->first < r.hi) ||
+                          (next != g_pins.begin() && std::prev(next)->second.hi > r.lo);
+    if (overlaps)
+      return fail(LBF_ERR_INVALID, "lbf_host_register: range overlaps, but differs from, one another context holds");
+    hipPointerAttribute_t attr{};
+    if (hipPointerGetAttributes(&attr, reinterpret_cast<void*>(r.lo)) == hipSuccess && attr.type == hipMemoryTypeHost) {
+      ctx->regs.push_back(r);  // pinned already by someone else: use it, never unpin it
+      return (int)LBF_OK;
+    }
+    (void)hipGetLastError();  // pageable memory is an error to that query
+    KeepCurrentDevice keep;
+    LBF_HIP_TRY(hipSetDevice(ctx->workers[0].device));
+    const hipError_t e = hipHostRegister(reinterpret_cast<void*>(r.lo), r.hi - r.lo, hipHostRegisterPortable);
+    if (e == hipErrorHostMemoryAlreadyRegistered) {
+      (void)hipGetLastError();
+    } else if (e != hipSuccess) {
+      return hip_fail(e, "hipHostRegister");
+    } else {
+      g_pins[r.lo] = Pin{r.hi, 1};
+      r.owned = true;
+    }
+    ctx->regs.push_back(r);
+    return (int)LBF_OK;
+  });
+}
+
+extern "C" int lbf_host_unregister(lbf_ctx* ctx, const void* ptr) {
+  if (!ctx || !ptr) return fail(LBF_ERR_INVALID, "lbf_host_unregister: null context/pointer");
+  std::lock_guard<std::mutex> lock(ctx->mu);  // no job is reading it
+  const uintptr_t a = reinterpret_cast<uintptr_t>(ptr);
+  for (size_t k = 0; k < ctx->regs.size(); ++k) {
+    if (ctx->regs[k].user != a) continue;
+    const Registered r = ctx->regs[k];
+    ctx->regs.erase(ctx->regs.begin() + (long)k);
+    return r.owned ? unpin(r.lo) : LBF_OK;
+  }
+  return fail(LBF_ERR_INVALID, "lbf_host_unregister: pointer was not registered with this context");
+}
 
 extern "C" int lbf_sha1_batch(lbf_ctx* ctx, const uint8_t* base, uint64_t base_len, const uint64_t* offsets,
                               const uint32_t* sizes, uint64_t n, uint8_t* out_digests, int flags) {

@@ -75,6 +75,7 @@ class ChunkHasher:
         check(lib.lbf_ctx_create(device_mask, ctypes.byref(h)))
         self._h = h
         self._lib = lib
+        self._registered = {}  # pointer -> array kept alive while pinned
 
     @property
     def num_devices(self) -> int:
@@ -95,6 +96,32 @@ class ChunkHasher:
         if self._h:
             self._lib.lbf_ctx_destroy(self._h)
             self._h = None
+        self._registered = {}
+
+    def staging_stats(self) -> dict:
+        """Cumulative chunk bytes sent through pinned staging / straight from
+        registered memory (lbf_ctx_staging_stats)."""
+        st, di = ctypes.c_uint64(0), ctypes.c_uint64(0)
+        check(self._lib.lbf_ctx_staging_stats(self._h, ctypes.byref(st), ctypes.byref(di)))
+        return {"staged": st.value, "direct": di.value}
+
+    # -- caller-pinned sources (lbf_host_register) ---------------------------
+    def register_host(self, data) -> None:
+        """Pin `data` (a contiguous numpy array / buffer) for this context:
+        batches over it then go to the GPU without the staging copy.  The array
+        is kept alive until unregister_host / close."""
+        if isinstance(data, np.ndarray) and not data.flags.c_contiguous:
+            raise ValueError("register_host: the array must be C-contiguous (a copy would be pinned instead)")
+        buf = _as_u8(data)
+        if buf.size == 0:
+            raise ValueError("register_host: empty buffer")
+        check(self._lib.lbf_host_register(self._h, buf.ctypes.data, buf.size))
+        self._registered[buf.ctypes.data] = buf
+
+    def unregister_host(self, data) -> None:
+        ptr = _as_u8(data).ctypes.data
+        check(self._lib.lbf_host_unregister(self._h, ptr))
+        self._registered.pop(ptr, None)
 
     def __enter__(self):
         return self

@@ -99,6 +99,28 @@ int lbf_verify_batch(lbf_ctx* ctx, const uint8_t* base, uint64_t base_len,
                      const uint64_t* offsets, const uint32_t* sizes, uint64_t n,
                      const uint8_t* expected, uint8_t* verdicts, int flags);
 
+/* ---- caller-pinned sources ------------------------------------------------
+ * Register [ptr, ptr + len) of caller host memory with the context (pinned
+ * for all of its devices; whole pages).  A LBF_HOST_PTR batch whose
+ * [base, base + base_len) lies in a registered range is copied to the device
+ * straight from it, one H2D per run of adjacent chunks, instead of passing
+ * through the context's pinned staging: host DRAM then carries each byte
+ * once, not three times (the staging memcpy's read and write, then the DMA
+ * read).  Groups of small scattered chunks (runs under 1 MiB on average),
+ * and jobs over 512 MiB per device, still go through staging: on one MI355X
+ * the direct route is ~15 % faster up to 256 MiB and ~15 % slower from 1 GiB
+ * (DESIGN.md §3).  Meant for buffers reused across calls (a peer's receive
+ * arenas, a resident file image); registering 4 GiB took ~6 ms.  Memory that is already pinned is accepted and left
+ * pinned.  Ranges held by one context may not overlap.  Unregister (with the
+ * pointer passed here) before freeing the memory; lbf_ctx_destroy unregisters
+ * what is left. */
+int lbf_host_register(lbf_ctx* ctx, const void* ptr, uint64_t len);
+int lbf_host_unregister(lbf_ctx* ctx, const void* ptr);
+/* Cumulative chunk bytes this context's host-pointer and file batches sent
+ * through its pinned staging and straight from registered memory
+ * (diagnostics; either pointer may be NULL). */
+int lbf_ctx_staging_stats(lbf_ctx* ctx, uint64_t* staged_bytes, uint64_t* direct_bytes);
+
 /* ---- chunks read straight from a file ------------------------------------
  * Chunk i = bytes [offsets[i], offsets[i] + sizes[i]) of the file at `path`,
  * read with pread into the context's pinned staging (no intermediate copy),
@@ -149,8 +171,10 @@ int lbf_sha1_uniform_launch(const uint8_t* d_base, uint64_t len, uint32_t chunk_
                             uint64_t first_chunk, uint64_t n, uint8_t* d_digests,
                             const uint8_t* d_expected, uint8_t* d_verdicts, void* stream);
 /* Kernel variant selection for the two launchers above (0 = automatic):
- * 1 lane, 2 pc, 3 lds, 4 pc2, 5 pcx2, 6 pc4, 7/8 pc4 with the schedule
- * read as 8-byte pairs, 9 pcx4, 10 pcx5, 11 lds2.  Exposed for benchmarking and tests; see
+ * shipped are 1 lane, 7 pc4 (schedule read as 8-byte pairs), 10 pcx5 and
+ * 11 lds2; the superseded 2 pc, 3 lds, 4 pc2, 5 pcx2, 6 pc4, 8 and 9 pcx4
+ * exist only in the LBF_EXPERIMENTAL_VARIANTS build, and the shipped library
+ * rejects them with LBF_ERR_INVALID.  Exposed for benchmarking and tests; see
  * DESIGN.md "kernels".  lbf_kernel_for(n) is the variant a launch of n
  * chunks runs under the current setting. */
 int lbf_set_kernel_variant(int variant);

@@ -1,0 +1,152 @@
+"""Caller-pinned sources (lbf_host_register): batches over registered host
+memory go to the GPU without the pinned-staging copy, and must give exactly
+what the staged path and the oracle give.
+
+The reference hashes from whatever buffer the caller holds
+(/root/reference/cpp/src/Encoder.cpp:107-120 on `new[]`/`malloc` buffers,
+Flood.cpp:263, ChunkMethods.cpp:113,159); registration only changes how the
+bytes reach HBM.  `staging_stats()` shows which route each byte took.
+"""
+import numpy as np
+import pytest
+
+from bitflood_amd import ChunkHasher, LbfError, chunk_table
+from bitflood_amd import _capi
+
+pytestmark = pytest.mark.gpu
+MIB = 1 << 20
+
+
+def _ctx(monkeypatch, **env):
+    with monkeypatch.context() as m:  # read at context creation only
+        for k, v in env.items():
+            m.setenv(k, str(v))
+        return ChunkHasher()
+
+
+def _delta(h, before):
+    now = h.staging_stats()
+    return {k: now[k] - before[k] for k in now}
+
+
+@pytest.mark.parametrize("workers", [1, 2])
+def test_registered_contiguous_hash_and_verify(workers, oracle, monkeypatch):
+    # 96 MiB + a ragged tail at 256 KiB chunks, several 16 MiB groups per worker
+    h = _ctx(monkeypatch, LBF_WORKERS_PER_DEVICE=workers, LBF_SLOT_MB=16)
+    try:
+        buf = oracle.synth(71, 0, 96 * MIB + 12345, nthreads=8)
+        offs, sizes = chunk_table(buf.size, 256 * 1024)
+        want = oracle.sha1_batch(buf, offs, sizes, nthreads=8)
+        h.register_host(buf)
+        s0 = h.staging_stats()
+        got = h.hash_chunks(buf, offs, sizes)
+        d = _delta(h, s0)
+        assert np.array_equal(got, want)
+        # every 16 MiB group direct; the last group holds only the 12,345-byte
+        # tail chunk, under the 1 MiB a direct copy needs, so it is staged
+        assert d["direct"] == buf.size - 12345 and d["staged"] == 12345, d
+        flips = [0, 7, 200, offs.size - 1]
+        exp = want.copy()
+        exp[flips, 19] ^= 1
+        v = h.verify_chunks(buf, offs, sizes, exp)
+        assert np.flatnonzero(~v).tolist() == flips
+        # unregistered: the same batch goes through staging, same digests
+        h.unregister_host(buf)
+        s1 = h.staging_stats()
+        assert np.array_equal(h.hash_chunks(buf, offs, sizes), want)
+        d = _delta(h, s1)
+        assert d["direct"] == 0 and d["staged"] == buf.size, d
+    finally:
+        h.close()
+
+
+def test_registered_mixed_groups(oracle, monkeypatch):
+    """One job whose groups take both routes: long contiguous runs go direct,
+    scattered small chunks (runs under 1 MiB on average) are staged, and
+    chunks larger than a slot take the oversize path."""
+    h = _ctx(monkeypatch, LBF_SLOT_MB=8)
+    try:
+        rng = np.random.default_rng(5)
+        buf = oracle.synth(72, 0, 64 * MIB, nthreads=8)
+        o1, s1 = chunk_table(32 * MIB, 1 * MIB)                        # contiguous: direct
+        s2 = rng.integers(0, 20000, 3000).astype(np.uint32)           # scattered: staged
+        o2 = np.sort(rng.integers(32 * MIB, 64 * MIB - 20000, 3000)).astype(np.uint64)
+        # oversize: batches grow to 16 MiB here (the long-chain rule), these do not fit
+        o3 = np.array([3 * MIB + 17, 40 * MIB], dtype=np.uint64)
+        s3 = np.array([17 * MIB, 20 * MIB + 5], dtype=np.uint32)
+        offs = np.concatenate([o1, o2, o3])
+        sizes = np.concatenate([s1, s2, s3])
+        want = oracle.sha1_batch(buf, offs, sizes, nthreads=8)
+        h.register_host(buf)
+        s0 = h.staging_stats()
+        got = h.hash_chunks(buf, offs, sizes)
+        d = _delta(h, s0)
+        bad = np.flatnonzero((got != want).any(axis=1))
+        assert bad.size == 0, bad[:10]
+        # the oversize chunk at 3 MiB splits the contiguous runs (4 MiB, then a
+        # full 16 MiB group, both direct); the group that ends them also takes
+        # scattered chunks, so it is staged
+        assert d["direct"] >= 16 * MIB and d["staged"] > 0, d
+        h.unregister_host(buf)
+    finally:
+        h.close()
+
+
+def test_registered_range_rules(oracle, monkeypatch):
+    h = _ctx(monkeypatch, LBF_SLOT_MB=8)
+    g = ChunkHasher()
+    try:
+        buf = oracle.synth(73, 0, 24 * MIB, nthreads=8)
+        offs, sizes = chunk_table(buf.size, 2 * MIB)
+        want = oracle.sha1_batch(buf, offs, sizes, nthreads=8)
+        mid = buf[8 * MIB:16 * MIB]
+        h.register_host(mid)
+        # a batch over the whole buffer is not inside the registered part: staged
+        s0 = h.staging_stats()
+        assert np.array_equal(h.hash_chunks(buf, offs, sizes), want)
+        assert _delta(h, s0)["direct"] == 0
+        # a batch over the registered part only: direct (offsets relative to it)
+        mo, ms = chunk_table(mid.size, 2 * MIB)
+        s0 = h.staging_stats()
+        assert np.array_equal(h.hash_chunks(mid, mo, ms), want[4:8])
+        assert _delta(h, s0)["direct"] == mid.size
+        # overlapping ranges in one context, unknown and repeated unregisters
+        with pytest.raises(LbfError) as e:
+            h.register_host(buf[12 * MIB:20 * MIB])
+        assert e.value.status == _capi.LBF_ERR_INVALID
+        with pytest.raises(LbfError):
+            h.unregister_host(buf)
+        # a second context may use memory the first one pinned: accepted, never unpinned by it
+        g.register_host(mid)
+        s0 = g.staging_stats()
+        assert np.array_equal(g.hash_chunks(mid, mo, ms), want[4:8])
+        assert _delta(g, s0)["direct"] == mid.size
+        g.unregister_host(mid)
+        assert np.array_equal(h.hash_chunks(mid, mo, ms), want[4:8])  # still pinned for h
+        h.unregister_host(mid)
+        with pytest.raises(LbfError):
+            h.unregister_host(mid)
+        # destroy with a registration outstanding (it is unpinned there), then
+        # a new context registers the same memory
+        h.register_host(buf)
+        h.close()
+        h = ChunkHasher()
+        h.register_host(buf)
+        assert np.array_equal(h.hash_chunks(buf, offs, sizes), want)
+    finally:
+        h.close()
+        g.close()
+
+
+def test_failed_hip_call_does_not_fail_the_next_one(oracle, hasher):
+    """A HIP call that fails leaves its status as the thread's last error;
+    the library reads it off when it reports the failure, so the next launch
+    (which checks hipGetLastError) is not failed by it.  Round 2 found this
+    when a failed hipHostUnregister failed the next test's kernel launch."""
+    import ctypes
+    lib = _capi.load()
+    bogus = ctypes.c_void_p(0x7F0000001000)  # no device allocation lives here
+    assert lib.lbf_dev_free(bogus) == _capi.LBF_ERR_HIP
+    buf = oracle.synth(74, 0, 1 << 20, nthreads=4)
+    offs, sizes = chunk_table(buf.size, 64 * 1024)
+    assert np.array_equal(hasher.hash_chunks(buf, offs, sizes), oracle.sha1_batch(buf, offs, sizes, nthreads=4))
