@@ -1216,7 +1216,9 @@ extern "C" int lbf_host_register(lbf_ctx* ctx, const void* ptr, uint64_t len) {
     std::lock_guard<std::mutex> lock(ctx->mu);
     for (const Registered& o : ctx->regs)
       if (r.lo < o.hi && o.lo < r.hi)
-        return fail(LBF_ERR_INVALID, "lbf_host_register: range overlaps one this context already holds");
+        return fail(LBF_ERR_INVALID,
+                    "lbf_host_register: range shares pages with one this context already holds (pinning is per "
+                    "page: give each registered buffer pages of its own)");
     ctx->regs.reserve(ctx->regs.size() + 1);  // nothing below may throw once pinned
     std::lock_guard<std::mutex> pins(g_pin_mu);
     auto next = g_pins.lower_bound(r.lo);

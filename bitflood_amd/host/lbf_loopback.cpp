@@ -73,6 +73,7 @@ struct Opts {
   std::string dir;
   bool keep = false;
   bool synthetic = false;
+  bool register_arenas = true;  // --no-register: stage the leecher's verifies (A/B)
 };
 
 [[noreturn]] void die(const std::string& m) {
@@ -466,10 +467,11 @@ int main(int argc, char** argv) {
     else if (a == "--dir") o.dir = val();
     else if (a == "--keep") o.keep = true;
     else if (a == "--synthetic") o.synthetic = true;
+    else if (a == "--no-register") o.register_arenas = false;
     else {
       fprintf(stderr,
               "usage: lbf_loopback [--size BYTES] [--chunksize N] [--window W] [--batch B] [--threads T]\n"
-              "                    [--corrupt K] [--dir DIR] [--keep] [--synthetic]\n");
+              "                    [--corrupt K] [--dir DIR] [--keep] [--synthetic] [--no-register]\n");
       return 2;
     }
   }
@@ -531,7 +533,29 @@ int main(int argc, char** argv) {
   const size_t total = todo.size();
   constexpr int kArenas = 3;
   const U64 slot = ((U64)o.chunksize + 15) & ~15ull;
-  std::vector<V_U8> arenas(kArenas, V_U8(slot * o.batch));
+  // The arenas live for the whole transfer: pinned once, each batch's verify
+  // copies them straight to HBM instead of through the context's staging
+  // (lbf_host_register; batches are far under its 512 MiB direct limit).
+  // Registration pins whole pages, so each arena starts on a page of its own.
+  const U64 page = (U64)sysconf(_SC_PAGESIZE);
+  const U64 arena_len = slot * o.batch, arena_stride = (arena_len + page - 1) / page * page;
+  U8* const arena_mem = static_cast<U8*>(aligned_alloc(page, arena_stride * kArenas));
+  if (!arena_mem) die("leecher: cannot allocate the arenas");
+  memset(arena_mem, 0, arena_stride * kArenas);
+  struct Arena {
+    U8* p;
+    U64 n;
+    U8* data() const { return p; }
+    U64 size() const { return n; }
+  };
+  std::vector<Arena> arenas;
+  for (int a = 0; a < kArenas; ++a) arenas.push_back(Arena{arena_mem + a * arena_stride, arena_len});
+  lbf_ctx* const leech_ctx = Encoder::Context();
+  if (!leech_ctx) die("leecher: no GPU context: " + std::string(Encoder::LastError()));
+  if (o.register_arenas)
+    for (const Arena& a : arenas)
+      if (lbf_host_register(leech_ctx, a.data(), a.size()) != LBF_OK)
+        die("leecher: lbf_host_register failed: " + std::string(lbf_last_error()));
   const int fd = connect_loopback(port);
 
   // Leecher pipeline: reader thread (frames), this thread (decode into one of
@@ -689,6 +713,9 @@ int main(int argc, char** argv) {
   const auto t_end = Clock::now();
   to_verify.close();
   verifier.join();
+  if (o.register_arenas)
+    for (const Arena& a : arenas) (void)lbf_host_unregister(leech_ctx, a.data());
+  free(arena_mem);
   shutdown(fd, SHUT_RDWR);
   reader.join();
   close(fd);
@@ -711,14 +738,15 @@ int main(int argc, char** argv) {
          "\"rejected\": %zu, \"undecodable\": %zu}, \"seeder\": {\"requests\": %llu, \"sent\": %llu, \"refused\": %llu, \"verify_s\": %.3f, "
          "\"encode_s\": %.3f}, \"verify_latency_us\": {\"p50\": %.0f, \"p90\": %.0f, \"p99\": %.0f, \"max\": %.0f}, "
          "\"resume_verify_complete\": %s, \"files_identical\": %s, \"corrupt_every\": %u, \"corrupted_sent\": %llu, "
-         "\"seed_source\": \"%s\"}\n",
+         "\"seed_source\": \"%s\", \"arenas_registered\": %s}\n",
          (unsigned long long)o.size, o.chunksize, total, o.window, o.batch, o.threads, wall,
          payload / wall / (1u << 30), wire_bytes / wall / (1u << 30), encode_s, batches,
          batches ? (double)(accepted + rejected) / batches : 0.0, decode_s, verify_s, rejected, undecodable,
          (unsigned long long)sst.requests, (unsigned long long)sst.sent, (unsigned long long)sst.refused, sst.verify_s,
          sst.encode_s, pct(0.5), pct(0.9), pct(0.99), lat_us.empty() ? 0.0 : lat_us.back(), resumed ? "true" : "false",
          same ? "true" : "false", o.corrupt, (unsigned long long)sst.corrupted,
-         o.synthetic ? "synthetic stream (generated on request, no seeder file)" : "file");
+         o.synthetic ? "synthetic stream (generated on request, no seeder file)" : "file",
+         o.register_arenas ? "true" : "false");
   if (!o.keep) {
     unlink((seeddir + "/" + name).c_str());
     unlink((leechdir + "/" + name).c_str());

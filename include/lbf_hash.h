@@ -110,10 +110,11 @@ int lbf_verify_batch(lbf_ctx* ctx, const uint8_t* base, uint64_t base_len,
  * and jobs over 512 MiB per device, still go through staging: on one MI355X
  * the direct route is ~15 % faster up to 256 MiB and ~15 % slower from 1 GiB
  * (DESIGN.md §3).  Meant for buffers reused across calls (a peer's receive
- * arenas, a resident file image); registering 4 GiB took ~6 ms.  Memory that is already pinned is accepted and left
- * pinned.  Ranges held by one context may not overlap.  Unregister (with the
- * pointer passed here) before freeing the memory; lbf_ctx_destroy unregisters
- * what is left. */
+ * arenas, a resident file image); registering 4 GiB took ~6 ms.  Memory
+ * that is already pinned is accepted and left pinned.  Pinning is per page:
+ * ranges held by one context may not share a page (give each registered
+ * buffer pages of its own).  Unregister (with the pointer passed here) before
+ * freeing the memory; lbf_ctx_destroy unregisters what is left. */
 int lbf_host_register(lbf_ctx* ctx, const void* ptr, uint64_t len);
 int lbf_host_unregister(lbf_ctx* ctx, const void* ptr);
 /* Cumulative chunk bytes this context's host-pointer and file batches sent

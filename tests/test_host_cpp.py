@@ -92,17 +92,20 @@ def test_loopback_needs_gpu():
     assert out.returncode == 2 and "no CPU fallback" in out.stderr
 
 
-def _loopback(tmp_path, size, cs, window, batch, corrupt, synthetic=False, threads=None, timeout=600):
+def _loopback(tmp_path, size, cs, window, batch, corrupt, synthetic=False, threads=None, timeout=600, register=True):
     args = [os.path.join(LIB, "lbf_loopback"), "--size", str(size), "--chunksize", str(cs), "--window", str(window),
             "--batch", str(batch), "--corrupt", str(corrupt), "--dir", str(tmp_path / "c5")]
     if synthetic:
         args.append("--synthetic")
     if threads:
         args += ["--threads", str(threads)]
+    if not register:
+        args.append("--no-register")
     out = subprocess.run(args, capture_output=True, text=True, timeout=timeout)
     assert out.returncode == 0, out.stderr + out.stdout
     r = json.loads(out.stdout.strip().splitlines()[-1])
     assert r["resume_verify_complete"] and r["files_identical"]
+    assert r["arenas_registered"] is register
     n = (size + cs - 1) // cs
     assert r["chunks"] == n
     if corrupt:
@@ -131,6 +134,14 @@ def test_loopback_two_peers(tmp_path, size, cs, window, batch, corrupt, syntheti
     equals the source (a file, or with --synthetic the generated stream) byte
     for byte."""
     _loopback(tmp_path, size, cs, window, batch, corrupt, synthetic)
+
+
+@pytest.mark.gpu
+def test_loopback_staged_arenas(tmp_path):
+    """The leecher's arenas are registered with its context by default, so its
+    verifies copy them straight to HBM (lbf_host_register); --no-register sends
+    them through the context's staging instead.  Same results either way."""
+    _loopback(tmp_path, (16 << 20) + 12345, 65536, 512, 128, 7, register=False)
 
 
 @pytest.mark.gpu
