@@ -49,7 +49,7 @@ int main(int argc, char** argv) {
   std::mt19937_64 rng(seed);
   auto uni = [&](uint64_t lo, uint64_t hi) { return lo + rng() % (hi - lo + 1); };
   const auto t_end = std::chrono::steady_clock::now() + std::chrono::duration<double>(budget);
-  long cases = 0, chunks_checked = 0, faults = 0;
+  long cases = 0, chunks_checked = 0, faults = 0, registered = 0;
   const std::string path = dir + "/asan_capi.bin";
 
   while (std::chrono::steady_clock::now() < t_end && g_fail == 0) {
@@ -85,6 +85,10 @@ int main(int argc, char** argv) {
       std::vector<uint8_t> want(20 * n), got(20 * n, 0xEE);
       for (uint64_t i = 0; i < n; ++i) oracle_sha1(buf.data() + off[i], size[i], &want[20 * i]);
       ++cases;
+      // half the jobs read from memory registered with the context (the direct route)
+      const bool reg = uni(0, 1) == 0;
+      if (reg) CHECK(lbf_host_register(ctx, buf.data(), buf_len) == LBF_OK, "register: %s", lbf_last_error());
+      registered += reg;
       int rc = lbf_sha1_batch(ctx, buf.data(), buf_len, off.data(), size.data(), n, got.data(), LBF_HOST_PTR);
       if (rc == LBF_ERR_HIP && strstr(lbf_last_error(), "injected fault")) {
         ++faults;  // one-shot: the same job must now succeed on the same context
@@ -111,6 +115,7 @@ int main(int argc, char** argv) {
       }
       CHECK(rc == LBF_OK, "verify rc %d: %s", rc, lbf_last_error());
       for (uint64_t i = 0; i < n && rc == LBF_OK; ++i) CHECK(ver[i] == (bad[i] ? 0 : 1), "verdict %lu", (unsigned long)i);
+      if (reg) CHECK(lbf_host_unregister(ctx, buf.data()) == LBF_OK, "unregister: %s", lbf_last_error());
       // the same chunks from a file, truncated in half of the cases
       const uint64_t keep = uni(0, 1) ? buf_len : uni(0, buf_len);
       const int fd = open(path.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
@@ -179,8 +184,8 @@ int main(int argc, char** argv) {
     lbf_ctx_destroy(ctx);
   }
   unlink(path.c_str());
-  std::printf("asan_capi %s: %ld cases, %ld chunks, %ld injected faults, seed %lu\n", g_fail ? "FAIL" : "OK", cases,
-              chunks_checked, faults, (unsigned long)seed);
+  std::printf("asan_capi %s: %ld cases (%ld from registered memory), %ld chunks, %ld injected faults, seed %lu\n",
+              g_fail ? "FAIL" : "OK", cases, registered, chunks_checked, faults, (unsigned long)seed);
   std::fflush(stdout);
   // Skip static destructors: the HIP runtime's own teardown (libamdhip64
   // __cxa_finalize) can trip ASan's device-allocator CHECK

@@ -4,8 +4,8 @@
 tools/fuzz_gpu.py varies the kernels; this varies what feeds them: staging slot
 sizes (1, 3, 16, 512 MiB, so batches split into many groups and chunks larger
 than a slot take the oversize path), chunk sizes up to 40 MiB, memory vs file
-sources (pread), truncated and missing files in verify mode, and device-pointer
-batches.  The copy-thread count is process-wide (LBF_COPY_THREADS), so run the
+sources (pread), truncated and missing files in verify mode, device-pointer
+batches, and memory registered with the context (the direct route).  The copy-thread count is process-wide (LBF_COPY_THREADS), so run the
 tool once per setting.  Everything is checked against the oracle restatement.
 
 Usage: LBF_COPY_THREADS=3 python tools/fuzz_host_paths.py [--seconds 60] [--seed 1]
@@ -54,11 +54,34 @@ def draw_table(rng, span):
     return offs, sizes
 
 
+def registered_case(rng, slot, mode, orc, h, pool):
+    start = int(rng.integers(0, 8192)) if rng.random() < 0.5 else 0
+    src = pool[start:]
+    offs, sizes = draw_table(rng, src.size)
+    want = orc.sha1_batch(src, offs, sizes, nthreads=THREADS)
+    n = offs.size
+    h.register_host(src)
+    try:
+        if mode == 5:
+            return slot, mode, n, bool(np.array_equal(h.hash_chunks(src, offs, sizes), want))
+        exp = want.copy()
+        bad = rng.random(n) < 0.1
+        exp[bad, rng.integers(0, 20)] ^= np.uint8(1 << int(rng.integers(0, 8)))
+        return slot, mode, n, bool(np.array_equal(h.verify_chunks(src, offs, sizes, exp), ~bad))
+    finally:
+        h.unregister_host(src)
+
+
 def one_case(seed, orc, hashers, pool, path, tmpdir):
     rng = np.random.default_rng(seed)
     slot = int(rng.choice(SLOTS_MB))
     h = hashers[slot]
-    mode = int(rng.integers(0, 5))  # 0 mem hash, 1 mem verify, 2 file hash, 3 file verify, 4 device ptrs
+    # 0 mem hash, 1 mem verify, 2 file hash, 3 file verify, 4 device ptrs,
+    # 5/6 mem hash/verify from a registered source (lbf_host_register) that
+    # starts at a random byte of the pool
+    mode = int(rng.integers(0, 7))
+    if mode >= 5:
+        return registered_case(rng, slot, mode, orc, h, pool)
     offs, sizes = draw_table(rng, pool.size)
     want = orc.sha1_batch(pool, offs, sizes, nthreads=THREADS)
     n = offs.size
