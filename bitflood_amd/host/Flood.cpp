@@ -262,7 +262,8 @@ Error::ErrorCode Flood::ReadVerifiedChunks(const std::vector<P_ChunkKey>& i_keys
   // one open per file, pread per chunk (ChunkMethods.cpp:105-115 fopen/fread per request)
   std::map<std::string, int> fds;
   for (size_t k = 0; k < n; ++k)
-    if (ok[k] && !fds.count(i_keys[k].first)) fds[i_keys[k].first] = open(PathOf(i_keys[k].first).c_str(), O_RDONLY);
+    if (ok[k] && !fds.count(i_keys[k].first))
+      fds[i_keys[k].first] = open(PathOf(i_keys[k].first).c_str(), O_RDONLY | O_CLOEXEC);
   parallel_for(n, io_threads(), [&](size_t k) {
     if (!ok[k]) return;
     const int fd = fds.find(i_keys[k].first)->second;
@@ -352,7 +353,7 @@ Error::ErrorCode Flood::ReceiveChunks(const U8* i_arena, U64 i_arena_len, const 
   std::map<std::string, int> fds;
   for (size_t k : which) {
     const std::string& name = i_chunks[k].m_filename;
-    if (!fds.count(name)) fds[name] = open(PathOf(name).c_str(), O_RDWR | O_CREAT, 0644);
+    if (!fds.count(name)) fds[name] = open(PathOf(name).c_str(), O_RDWR | O_CREAT | O_CLOEXEC, 0644);
   }
   std::vector<U8> written(which.size(), 0);
   parallel_for(which.size(), io_threads(), [&](size_t j) {
