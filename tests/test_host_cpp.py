@@ -2,9 +2,11 @@
 the resume-verify CLI (GPU), and the C++ API tests in lbf_gpu_tests (GPU).
 
 Expected flood-file bytes are built here from the golden chunk strings with the
-Xerces 2.6 DOMWriter pretty-print rules (see bitflood_amd/host/FloodFile.cpp
-for the DOMWriterImpl.cpp citations).  No reference run pins those bytes: the
-format is pinned by code reading.
+Xerces 2.6 DOMWriter pretty-print restatement of tests/domwriter.py, whose
+layout rules tests/test_floodfile_format.py pins against Xerces' own expected
+output (a fixture the reference holds).  No flood file exists in the
+reference, so attribute order and escaping rest on code reading (SURVEY.md §4,
+§8f).
 """
 import base64
 import json
@@ -16,6 +18,7 @@ import numpy as np
 import pytest
 
 from bitflood_amd import _capi
+from tests.domwriter import pretty
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "bitflood_amd", "lib")
@@ -23,30 +26,18 @@ ENCODER = os.path.join(LIB, "lbf_encoder")
 VERIFY = os.path.join(LIB, "lbf_verify")
 
 
-def _escape(v: str) -> str:
-    return v.replace("&", "&amp;").replace("<", "&lt;").replace('"', "&quot;").replace("\n", "&#xA;")
-
-
 def expected_xml(files, trackers) -> str:
-    """files: list of (name, size, [(hash, index, size, weight)]) in map order."""
-    x = "\n<BitFlood>\n\n  <FileInfo"
-    if not files:
-        x += "/>"
-    else:
-        x += ">"
-        for name, size, chunks in sorted(files, key=lambda f: f[0].encode()):
-            x += f'\n    <File name="{_escape(name)}" size="{size}"'
-            if not chunks:
-                x += "/>"
-                continue
-            x += ">"
-            for h, i, s, w in chunks:
-                x += f'\n      <Chunk hash="{_escape(h)}" index="{i}" size="{s}" weight="{w}"/>'
-            x += "\n    </File>"
-        x += "\n  </FileInfo>"
-    for host, port in trackers:
-        x += f'\n\n  <Tracker host="{_escape(host)}" port="{port}"/>'
-    return x + "\n\n</BitFlood>"
+    """files: list of (name, size, [(hash, index, size, weight)]) in map order.
+    The tree FloodFile::ToXML builds (FloodFile.cpp:42-142), written by the
+    DOMWriter restatement that tests/test_floodfile_format.py pins against
+    Xerces' own expected output; attributes in name order."""
+    file_nodes = []
+    for name, size, chunks in sorted(files, key=lambda f: f[0].encode()):
+        kids = [("Chunk", [("hash", h), ("index", str(i)), ("size", str(s)), ("weight", str(w))], [])
+                for h, i, s, w in chunks]
+        file_nodes.append(("File", [("name", name), ("size", str(size))], kids))
+    tracker_nodes = [("Tracker", [("host", host), ("port", str(port))], []) for host, port in trackers]
+    return pretty(("BitFlood", [], [("FileInfo", [], file_nodes)] + tracker_nodes))
 
 
 def b64_27(d: bytes) -> str:
