@@ -8,9 +8,11 @@ as data by tests/golden/make_xerces_fixture.py.  Every element-only document
 there must come out of the restatement (tests/domwriter.py) byte for byte;
 the C++ writer is then checked against the same restatement
 (tests/test_host_cpp.py, host_tests.cpp).  This pins the layout -- newlines,
-indentation, blank lines, "/>" -- by the reference's own fixture; attribute
-order and escaping stay pinned by code reading (none of these documents sorts
-or escapes).
+indentation, blank lines, "/>" -- by the reference's own fixture.  The
+attribute order follows from the reference's setAttribute calls, which are in
+name order already (FloodFile.cpp:74-75,95-98,115-116), so sorted and
+insertion order agree; only the escapes rest on code reading (no fixture holds
+a character that needs one).
 """
 import json
 import os
