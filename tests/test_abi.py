@@ -36,6 +36,17 @@ def test_abi_version():
     assert _capi.load().lbf_abi_version() == 1
 
 
+def test_b64_27_product_matches_cryptopp_vector():
+    """The product's rendering (lbf_b64_27, host code of liblbfhash.so) and its
+    inverse against Crypto++ 5.2.1's own expected base64 output
+    (tests/test_oracle.py explains which 20-byte windows it pins)."""
+    from bitflood_amd import b64_27, b64_27_decode
+    from tests.test_oracle import cryptopp_windows
+    for d, want in cryptopp_windows():
+        assert b64_27(d) == want
+        assert b64_27_decode(want) == d
+
+
 def test_b64_27_host_formatting_matches_python():
     from bitflood_amd import b64_27, b64_27_decode
     rng = np.random.default_rng(5)

@@ -1,17 +1,21 @@
 """Pin the CPU oracle (oracle/sha1_oracle.c) before trusting it as the checker.
 
 Anchors: Crypto++ SHA-1 KATs (cpp/extern/crypto++/5.2.1/TestVectors/sha.txt:1-11),
-hashlib-generated golden fixtures (tests/golden/make_golden.py), and Python's
-base64 for the 27-char rendering (basecode.cpp:39-104 without padding).
+hashlib-generated golden fixtures (tests/golden/make_golden.py), and for the
+27-char rendering (basecode.cpp:39-104 without padding) Crypto++'s own expected
+base64 output (validat1.cpp ValidateBaseCode, tests/golden/cryptopp521_base64.json)
+plus Python's base64.
 """
 import base64
 import hashlib
+import json
 import os
 
 import numpy as np
 import pytest
 
 SEED_C = 0x5EED
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
 def _kat_message(k):
@@ -50,6 +54,33 @@ def test_incremental_update_matches_one_shot(oracle):
         for _ in range(3):
             splits = sorted(rng.integers(0, n + 1, size=int(rng.integers(0, 6))).tolist())
             assert oracle.sha1_incremental(data, splits) == want
+
+
+def _cryptopp_base64_stream():
+    """Crypto++ 5.2.1's own expected Base64Encoder output for bytes 0..254
+    (validat1.cpp, ValidateBaseCode; tests/golden/make_cryptopp_base64_fixture.py),
+    line breaks removed."""
+    with open(os.path.join(GOLDEN, "cryptopp521_base64.json")) as f:
+        return json.load(f)["base64_with_linebreaks"].replace("\n", "")
+
+
+def cryptopp_windows():
+    """20-byte windows of bytes 0..254 whose 27-char rendering is a slice of
+    Crypto++'s own expected output: the window must start on a 3-byte group
+    (chars 4k..) and the byte after it must be < 64, so that the 27th char of
+    the stream carries the window's last 4 bits followed by two zero bits, as
+    the unpadded 27th char does (basecode.cpp:39-104)."""
+    s = _cryptopp_base64_stream()
+    return [(bytes(range(3 * k, 3 * k + 20)), s[4 * k:4 * k + 27]) for k in range(15) if 3 * k + 20 < 64]
+
+
+def test_b64_27_restatement_matches_cryptopp_vector(oracle):
+    w = cryptopp_windows()
+    assert len(w) == 15
+    for d, want in w:
+        assert oracle.b64_27(d) == want
+    # and the stream itself is what Python's codec gives for 0..254
+    assert _cryptopp_base64_stream() == base64.b64encode(bytes(range(255))).decode()
 
 
 def test_b64_27_restatement(oracle):
