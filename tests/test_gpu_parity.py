@@ -53,6 +53,24 @@ def test_kats(variant, hasher, golden):
         assert hasher.base64_encode(m) == k["b64_27"], k["name"]
 
 
+def test_hmac_sha1_kats_through_batches(variant, hasher):
+    """Crypto++'s HMAC(SHA-1) known answers (TestVectors/hmac.txt) as three
+    batched SHA-1 passes on the GPU: each message of a stage packed back to
+    back in one buffer at its natural, unaligned offset."""
+    from tests.test_oracle import hmac_sha1_cases
+
+    def sha1_many(msgs):
+        if not msgs:
+            return []
+        buf = np.frombuffer(b"".join(msgs), dtype=np.uint8)
+        sizes = np.array([len(m) for m in msgs], dtype=np.uint32)
+        offs = np.concatenate([[0], np.cumsum(sizes[:-1], dtype=np.uint64)]).astype(np.uint64)
+        return list(hasher.hash_chunks(buf, offs, sizes))
+
+    for name, got, want in hmac_sha1_cases(sha1_many):
+        assert got == want, name
+
+
 def test_tails(variant, hasher, oracle, golden):
     for t in golden("synthetic.json")["tails"]:
         data = oracle.synth(t["seed"], 0, t["size"])

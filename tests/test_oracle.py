@@ -1,6 +1,7 @@
 """Pin the CPU oracle (oracle/sha1_oracle.c) before trusting it as the checker.
 
-Anchors: Crypto++ SHA-1 KATs (cpp/extern/crypto++/5.2.1/TestVectors/sha.txt:1-11),
+Anchors: Crypto++ SHA-1 KATs (cpp/extern/crypto++/5.2.1/TestVectors/sha.txt:1-11)
+and its HMAC(SHA-1) KATs (TestVectors/hmac.txt, two SHA-1 passes each),
 hashlib-generated golden fixtures (tests/golden/make_golden.py), and for the
 27-char rendering (basecode.cpp:39-104 without padding) Crypto++'s own expected
 base64 output (validat1.cpp ValidateBaseCode, tests/golden/cryptopp521_base64.json)
@@ -81,6 +82,31 @@ def test_b64_27_restatement_matches_cryptopp_vector(oracle):
         assert oracle.b64_27(d) == want
     # and the stream itself is what Python's codec gives for 0..254
     assert _cryptopp_base64_stream() == base64.b64encode(bytes(range(255))).decode()
+
+
+def hmac_sha1_cases(sha1_many):
+    """Crypto++'s HMAC(SHA-1) known answers (TestVectors/hmac.txt, RFC 2202;
+    tests/golden/make_cryptopp_hmac_fixture.py) computed through `sha1_many`
+    (list of messages -> list of 20-byte digests): SHA-1 of a long key, then
+    SHA1((K ^ ipad) || m) and SHA1((K ^ opad) || inner), each stage one batch.
+    Returns [(name, got, want)]."""
+    with open(os.path.join(GOLDEN, "cryptopp521_hmac_sha1.json")) as f:
+        cases = json.load(f)["cases"]
+    keys = [bytes.fromhex(c["key"]) for c in cases]
+    long_ = [i for i, k in enumerate(keys) if len(k) > 64]
+    for i, d in zip(long_, sha1_many([keys[i] for i in long_])):
+        keys[i] = bytes(d)
+    keys = [k.ljust(64, b"\0") for k in keys]
+    inner = sha1_many([bytes(b ^ 0x36 for b in k) + bytes.fromhex(c["message"]) for k, c in zip(keys, cases)])
+    outer = sha1_many([bytes(b ^ 0x5C for b in k) + bytes(d) for k, d in zip(keys, inner)])
+    return [(c["name"], bytes(o).hex(), c["digest"]) for c, o in zip(cases, outer)]
+
+
+def test_oracle_reproduces_cryptopp_hmac_sha1_kats(oracle):
+    got = hmac_sha1_cases(lambda ms: [oracle.sha1(m) for m in ms])
+    assert len(got) == 7
+    for name, g, want in got:
+        assert g == want, name
 
 
 def test_b64_27_restatement(oracle):
