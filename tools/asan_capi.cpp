@@ -7,7 +7,11 @@
 //   lbf_sha1_batch / lbf_verify_batch (host memory) and
 //   lbf_file_ranges (hash and verify, including a truncated file) and
 //   lbf_files_ranges (verify over 2-4 truncated or missing files)
-// against the oracle (oracle/sha1_oracle.c, compiled in as the checker).
+// against the oracle (oracle/sha1_oracle.c, compiled in as the checker).  Half
+// the jobs read from memory registered with the context, and half the
+// contexts then take three concurrent callers with 24-40 MiB batches (enough
+// for the staging-copy helper threads), so a ThreadSanitizer build of the
+// same driver (tools/tsan_build.sh) sees every host thread the pipeline runs.
 //   asan_capi <scratch-dir> [seconds] [seed]
 #include <fcntl.h>
 #include <unistd.h>
@@ -16,8 +20,10 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
 #include <random>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "lbf_hash.h"
@@ -27,7 +33,7 @@ void oracle_sha1(const uint8_t* data, uint32_t len, uint8_t out[20]);
 void oracle_synth_fill_mt(uint8_t* out, uint64_t len, uint64_t seed, uint64_t start, int nthreads);
 }
 
-static int g_fail = 0;
+static std::atomic<int> g_fail{0};
 #define CHECK(cond, ...)                                                  \
   do {                                                                    \
     if (!(cond)) {                                                        \
@@ -49,10 +55,10 @@ int main(int argc, char** argv) {
   std::mt19937_64 rng(seed);
   auto uni = [&](uint64_t lo, uint64_t hi) { return lo + rng() % (hi - lo + 1); };
   const auto t_end = std::chrono::steady_clock::now() + std::chrono::duration<double>(budget);
-  long cases = 0, chunks_checked = 0, faults = 0, registered = 0;
+  long cases = 0, chunks_checked = 0, faults = 0, registered = 0, concurrent = 0;
   const std::string path = dir + "/asan_capi.bin";
 
-  while (std::chrono::steady_clock::now() < t_end && g_fail == 0) {
+  while (std::chrono::steady_clock::now() < t_end && g_fail.load() == 0) {
     // ---- context shape (environment read at creation) ----
     const int workers = (int)uni(1, 4), slots = (int)uni(2, 5), slot_mb = (int)(uni(0, 3) == 0 ? 1 : uni(2, 16));
     const bool fault = uni(0, 4) == 0;
@@ -181,11 +187,51 @@ int main(int argc, char** argv) {
       }
       for (uint32_t f = 0; f < nf; ++f) unlink(fpaths[f].c_str());
     }
+    if (uni(0, 1) == 0) {
+      // three concurrent callers on this context (calls serialize on its
+      // mutex; each runs the multi-worker split and the copy helpers inside)
+      std::vector<uint64_t> seeds(3);
+      for (uint64_t& x : seeds) x = rng();
+      std::atomic<long> done_chunks{0}, done_faults{0};
+      std::vector<std::thread> callers;
+      for (int t = 0; t < 3; ++t)
+        callers.emplace_back([&, t] {
+          std::mt19937_64 r(seeds[t]);
+          auto u = [&](uint64_t lo, uint64_t hi) { return lo + r() % (hi - lo + 1); };
+          const uint64_t len = u(24, 40) << 20;
+          std::vector<uint8_t> b(len);
+          oracle_synth_fill_mt(b.data(), len, r(), 0, 2);
+          const uint64_t cs = u(0, 1) ? 262144 : u(1, 3) << 20;
+          const uint64_t n = (len + cs - 1) / cs;
+          std::vector<uint64_t> o(n);
+          std::vector<uint32_t> z(n);
+          for (uint64_t i = 0; i < n; ++i) o[i] = i * cs, z[i] = (uint32_t)std::min<uint64_t>(cs, len - i * cs);
+          std::vector<uint8_t> w(20 * n), g(20 * n, 0xEE);
+          for (uint64_t i = 0; i < n; ++i) oracle_sha1(b.data() + o[i], z[i], &w[20 * i]);
+          const bool rg = u(0, 1) == 0;
+          if (rg) CHECK(lbf_host_register(ctx, b.data(), len) == LBF_OK, "register: %s", lbf_last_error());
+          int rc = lbf_sha1_batch(ctx, b.data(), len, o.data(), z.data(), n, g.data(), LBF_HOST_PTR);
+          if (rc == LBF_ERR_HIP && strstr(lbf_last_error(), "injected fault")) {
+            ++done_faults;
+            rc = lbf_sha1_batch(ctx, b.data(), len, o.data(), z.data(), n, g.data(), LBF_HOST_PTR);
+          }
+          CHECK(rc == LBF_OK, "concurrent hash rc %d: %s", rc, lbf_last_error());
+          CHECK(rc != LBF_OK || memcmp(g.data(), w.data(), 20 * n) == 0, "concurrent digests (caller %d)", t);
+          if (rg) CHECK(lbf_host_unregister(ctx, b.data()) == LBF_OK, "unregister: %s", lbf_last_error());
+          done_chunks += (long)n;
+        });
+      for (auto& c : callers) c.join();
+      chunks_checked += done_chunks.load();
+      faults += done_faults.load();
+      cases += 3;
+      concurrent += 3;
+    }
     lbf_ctx_destroy(ctx);
   }
   unlink(path.c_str());
-  std::printf("asan_capi %s: %ld cases (%ld from registered memory), %ld chunks, %ld injected faults, seed %lu\n",
-              g_fail ? "FAIL" : "OK", cases, registered, chunks_checked, faults, (unsigned long)seed);
+  std::printf("asan_capi %s: %ld cases (%ld from registered memory, %ld concurrent callers), %ld chunks, "
+              "%ld injected faults, seed %lu\n",
+              g_fail ? "FAIL" : "OK", cases, registered, concurrent, chunks_checked, faults, (unsigned long)seed);
   std::fflush(stdout);
   // Skip static destructors: the HIP runtime's own teardown (libamdhip64
   // __cxa_finalize) can trip ASan's device-allocator CHECK
