@@ -404,13 +404,31 @@ struct lbf_ctx {
 namespace {
 
 // Pinned host memory on the worker's NUMA node (hipHostMallocNumaUser makes
-// the allocation follow the calling thread's memory policy).
+// the allocation follow the calling thread's memory policy).  Allocations and
+// frees of pinned memory pass one process-wide mutex.  The HIP runtime is
+// thread-safe on its own; the mutex makes a context's teardown visibly happen
+// before another context reuses the same pinned pages, which is what a
+// ThreadSanitizer build (tools/tsan_build.sh) needs to see: it cannot look
+// inside the uninstrumented runtime's allocator, and reported the reuse of a
+// destroyed context's pages by the next one as a race.
+std::mutex g_pinned_mu;
+
 hipError_t host_alloc(const Worker& w, void** p, uint64_t bytes) {
   if (w.numa_node >= 0) {
     PreferNode pref(w.numa_node);
-    if (pref.active) return hipHostMalloc(p, bytes, hipHostMallocNumaUser);
+    if (pref.active) {
+      std::lock_guard<std::mutex> lock(g_pinned_mu);
+      return hipHostMalloc(p, bytes, hipHostMallocNumaUser);
+    }
   }
+  std::lock_guard<std::mutex> lock(g_pinned_mu);
   return hipHostMalloc(p, bytes, hipHostMallocDefault);
+}
+
+void host_free(void* p) {
+  if (!p) return;
+  std::lock_guard<std::mutex> lock(g_pinned_mu);
+  (void)hipHostFree(p);  // release paths: a failure has nowhere to go
 }
 
 int dev_slot_init(Worker& w, DevSlot& d) {
@@ -428,8 +446,8 @@ void dev_slot_free(DevSlot& d) {
   if (d.stream) (void)hipStreamSynchronize(d.stream);
   if (d.d_buf) (void)hipFree(d.d_buf);
   if (d.d_out) (void)hipFree(d.d_out);
-  if (d.h_out) (void)hipHostFree(d.h_out);
-  if (d.h_hdr) (void)hipHostFree(d.h_hdr);
+  host_free(d.h_out);
+  host_free(d.h_hdr);
   if (d.stream) (void)hipStreamDestroy(d.stream);
   d = DevSlot{};
 }
@@ -459,7 +477,7 @@ int ensure_slot_bytes(Worker& w, uint64_t need, uint64_t dev_cap) {
   if (pin_need > w.pin_bytes) {
     for (DevSlot& d : w.dev) LBF_HIP_TRY(hipStreamSynchronize(d.stream));  // no H2D reads a host slot
     for (HostSlot& h : w.host) {
-      if (h.h_buf) (void)hipHostFree(h.h_buf);
+      host_free(h.h_buf);
       h.h_buf = nullptr;
       h.in_flight = false;
     }
@@ -552,7 +570,7 @@ void worker_free(Worker& w) {
   for (DevSlot& d : w.dev) dev_slot_free(d);
   w.dev.clear();
   for (HostSlot& h : w.host) {
-    if (h.h_buf) (void)hipHostFree(h.h_buf);
+    host_free(h.h_buf);
     if (h.copied) (void)hipEventDestroy(h.copied);
     h = HostSlot{};
   }

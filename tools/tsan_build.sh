@@ -6,7 +6,8 @@
 # The driver's contexts run 1-4 workers, each with its own host thread and
 # staging-copy helper threads, so the races it can find are the host
 # pipeline's own.  Run on the GPU box:
-#   TSAN_OPTIONS="halt_on_error=1 report_signal_unsafe=0" tools/build/tsan/tsan_capi <scratch> [seconds] [seed]
+#   TSAN_OPTIONS="halt_on_error=1 report_signal_unsafe=0 suppressions=tools/tsan.supp" \
+#     tools/build/tsan/tsan_capi <scratch> [seconds] [seed]
 set -euo pipefail
 cd "$(dirname "$0")/.."
 OUT=tools/build/tsan
@@ -21,3 +22,12 @@ gcc -O2 -fPIC -c -o $OUT/sha1_oracle.o oracle/sha1_oracle.c -Ioracle
 $HIPCC --offload-arch=gfx950 $SAN -o $OUT/tsan_capi $OUT/tsan_capi.o $OUT/lbf_capi.o $OUT/sha1_kernels.o \
   $OUT/sha1_oracle.o -lpthread
 echo "built $OUT/tsan_capi"
+# the C++ libBitFlood layer and its GPU test program (8 threads on Base64Encode,
+# SetDeviceMask under 4 hashing threads, the Flood verify paths) on the same
+# instrumented C ABI:  tools/build/tsan/tsan_gpu_tests <scratch>
+for f in Encoder FloodFile Flood PeerWire gpu_tests; do
+  $HIPCC -O1 -g -std=c++17 -fPIC -Iinclude $SAN -c -o $OUT/$f.o bitflood_amd/host/$f.cpp
+done
+$HIPCC --offload-arch=gfx950 $SAN -o $OUT/tsan_gpu_tests $OUT/gpu_tests.o $OUT/Encoder.o $OUT/FloodFile.o \
+  $OUT/Flood.o $OUT/PeerWire.o $OUT/lbf_capi.o $OUT/sha1_kernels.o -lpthread
+echo "built $OUT/tsan_gpu_tests"
