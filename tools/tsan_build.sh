@@ -31,3 +31,9 @@ done
 $HIPCC --offload-arch=gfx950 $SAN -o $OUT/tsan_gpu_tests $OUT/gpu_tests.o $OUT/Encoder.o $OUT/FloodFile.o \
   $OUT/Flood.o $OUT/PeerWire.o $OUT/lbf_capi.o $OUT/sha1_kernels.o -lpthread
 echo "built $OUT/tsan_gpu_tests"
+# the C5 harness (reader, decode, verifier and sender threads of two peers):
+#   tools/build/tsan/tsan_loopback --size N --dir <scratch> ...
+$HIPCC -O1 -g -std=c++17 -fPIC -Iinclude $SAN -c -o $OUT/lbf_loopback.o bitflood_amd/host/lbf_loopback.cpp
+$HIPCC --offload-arch=gfx950 $SAN -o $OUT/tsan_loopback $OUT/lbf_loopback.o $OUT/Encoder.o $OUT/FloodFile.o \
+  $OUT/Flood.o $OUT/PeerWire.o $OUT/lbf_capi.o $OUT/sha1_kernels.o -lpthread
+echo "built $OUT/tsan_loopback"
