@@ -858,7 +858,9 @@ int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
       if (int rc = ensure_dev_slots(w, largest, groups)) return rc;
     }
   }
-  const bool direct_job = job.src.pinned && job_bytes <= kDirectMaxJob;
+  // LBF_DIRECT_MAX_MB: test/A-B knob for the size rule (read per job)
+  const uint64_t direct_max = (uint64_t)env_u64("LBF_DIRECT_MAX_MB", kDirectMaxJob >> 20) << 20;
+  const bool direct_job = job.src.pinned && job_bytes <= direct_max;
   int cur = 0, hcur = 0;
   uint64_t i = begin;
   int rc = LBF_OK;
@@ -934,11 +936,18 @@ int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
       uint8_t* h_header = nullptr;
       for (Run& r : runs) r.avail = 0;
       if (direct) {
+        // Runs go as copies of at most 32 MiB (LBF_DIRECT_PIECE_MB, an A/B knob; 0 = one copy per
+        // run): with every group direct, 4 GiB jobs ran at 47.2 GiB/s so against 42.5 as whole
+        // runs, 1 GiB at 39.6 against 35.4 (profiles/r02/registered_trace/piece_sweep/).
+        const uint64_t piece = env_u64("LBF_DIRECT_PIECE_MB", 32) << 20;
         for (Run& r : runs) {
-          if (!hip_ok(hipMemcpyAsync(s.d_buf + data_off + r.dst, job.src.base + r.src, r.len, hipMemcpyHostToDevice,
-                                     s.stream),
-                      "hipMemcpyAsync(H2D, registered source)"))
-            break;
+          const uint64_t step = piece ? piece : r.len;
+          for (uint64_t at = 0; at < r.len && rc == LBF_OK; at += step)
+            if (!hip_ok(hipMemcpyAsync(s.d_buf + data_off + r.dst + at, job.src.base + r.src + at,
+                                       std::min(step, r.len - at), hipMemcpyHostToDevice, s.stream),
+                        "hipMemcpyAsync(H2D, registered source)"))
+              break;
+          if (rc) break;
           r.avail = r.len;
         }
       }
