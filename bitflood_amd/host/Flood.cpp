@@ -258,7 +258,8 @@ Error::ErrorCode Flood::ReadVerifiedChunks(const std::vector<P_ChunkKey>& i_keys
     total += (c.m_size + 15) & ~15ull;  // keep every chunk 16-byte aligned in the arena
     ok[k] = 1;
   }
-  o_arena.assign(total ? total : 1, 0);
+  // grown, never cleared: every byte the verify reads is pread first
+  if (o_arena.size() < std::max<U64>(total, 1)) o_arena.resize(std::max<U64>(total, 1));
   // one open per file, pread per chunk (ChunkMethods.cpp:105-115 fopen/fread per request)
   std::map<std::string, int> fds;
   for (size_t k = 0; k < n; ++k)

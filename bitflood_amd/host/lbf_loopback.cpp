@@ -366,9 +366,24 @@ void seeder_main(int lfd, FloodFileSPtr ff, std::string root, const Opts& o, See
   });
   std::vector<Flood::P_ChunkKey> keys;
   Flood::S_ChunkKey corrupted;
+  // One arena for the whole transfer, page-aligned and (unless --no-register)
+  // registered with the seeder's context, like the leecher's: a batch costs no
+  // allocation, no zero fill of up to batch x chunk bytes, and no staging copy
+  // on its verify.  ReadVerifiedChunks keeps its own vector the same way.
+  const U64 page = (U64)sysconf(_SC_PAGESIZE);
+  const U64 slot_bytes = ((U64)o.chunksize + 15) & ~15ull;
+  const U64 synth_cap = (slot_bytes * o.batch + page - 1) / page * page;
+  U8* synth_arena = nullptr;
+  if (o.synthetic) {
+    synth_arena = static_cast<U8*>(aligned_alloc(page, synth_cap));
+    if (!synth_arena) die("seeder: cannot allocate the arena");
+    memset(synth_arena, 0, synth_cap);
+    if (o.register_arenas && lbf_host_register(ctx, synth_arena, synth_cap) != LBF_OK)
+      die("seeder: lbf_host_register failed: " + std::string(lbf_last_error()));
+  }
+  V_U8 file_arena;
   while (requests.take(keys, o.batch)) {
     st.requests += keys.size();
-    V_U8 arena;
     V_U64 offs;
     std::string valid;
     auto t0 = Clock::now();
@@ -387,17 +402,18 @@ void seeder_main(int lfd, FloodFileSPtr ff, std::string root, const Opts& o, See
         chunks[k] = Flood::ChunkArrival{keys[k].first, keys[k].second, total, sz};
         total += (sz + 15) & ~15ull;
       }
-      arena.assign(total ? total : 1, 0);
+      if (total > synth_cap) die("seeder: batch larger than its arena");
       parallel_for(keys.size(), o.threads, [&](size_t k) {
         auto it = fl.m_runtimefiles.find(keys[k].first);
         if (chunks[k].m_size == 0 || it == fl.m_runtimefiles.end()) return;
-        synth_bytes(&arena[offs[k]], it->second.m_chunkoffsets[keys[k].second], chunks[k].m_size);
+        synth_bytes(synth_arena + offs[k], it->second.m_chunkoffsets[keys[k].second], chunks[k].m_size);
       });
-      if (fl.VerifyChunks(arena.data(), arena.size(), chunks, valid) != Error::NO_ERROR_LBF)
+      if (fl.VerifyChunks(synth_arena, synth_cap, chunks, valid) != Error::NO_ERROR_LBF)
         die("seeder: verify failed: " + std::string(Encoder::LastError()));
-    } else if (fl.ReadVerifiedChunks(keys, arena, offs, valid) != Error::NO_ERROR_LBF) {
+    } else if (fl.ReadVerifiedChunks(keys, file_arena, offs, valid) != Error::NO_ERROR_LBF) {
       die("seeder: verify failed: " + std::string(Encoder::LastError()));
     }
+    const U8* arena = o.synthetic ? synth_arena : file_arena.data();
     auto t1 = Clock::now();
     // sizes and the (first-send-only) corruption decision, serially
     std::vector<U32> sizes(keys.size(), 0);
@@ -413,7 +429,7 @@ void seeder_main(int lfd, FloodFileSPtr ff, std::string root, const Opts& o, See
     std::vector<std::string> out(keys.size());
     parallel_for(keys.size(), o.threads, [&](size_t k) {
       if (valid[k] != '1') return;  // "send only if equal" (ChunkMethods.cpp:117-123)
-      const U8* data = &arena[offs[k]];
+      const U8* data = arena + offs[k];
       std::vector<U8> tmp;
       if (flip[k]) {  // a wire error after the seeder's own verify
         tmp.assign(data, data + sizes[k]);
@@ -438,6 +454,10 @@ void seeder_main(int lfd, FloodFileSPtr ff, std::string root, const Opts& o, See
   sender.join();
   reader.join();
   close(fd);
+  if (synth_arena) {
+    if (o.register_arenas) (void)lbf_host_unregister(ctx, synth_arena);
+    free(synth_arena);
+  }
   lbf_ctx_destroy(ctx);
 }
 
