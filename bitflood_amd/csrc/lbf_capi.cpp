@@ -358,6 +358,7 @@ struct DevSlot {
   uint8_t* d_out = nullptr;  // desc_cap * 20: digests, or verdicts
   uint8_t* h_out = nullptr;  // pinned
   std::vector<uint8_t> ok;   // 1 = chunk bytes fully available
+  hipEvent_t copied = nullptr;  // recorded after a direct-route batch's last H2D (see worker_run)
   // pending group (positions [g_begin, g_end)) to finalize after the stream drains
   bool pending = false;
   uint64_t g_begin = 0, g_end = 0;
@@ -437,6 +438,7 @@ int dev_slot_init(Worker& w, DevSlot& d) {
   LBF_HIP_TRY(host_alloc(w, (void**)&d.h_out, w.desc_cap * 20));
   LBF_HIP_TRY(host_alloc(w, (void**)&d.h_hdr, w.hdr_cap));
   if (w.slot_bytes) LBF_HIP_TRY(hipMalloc((void**)&d.d_buf, w.hdr_cap + w.slot_bytes));
+  LBF_HIP_TRY(hipEventCreateWithFlags(&d.copied, hipEventDisableTiming));
   d.ok.assign(w.desc_cap, 0);
   return LBF_OK;
 }
@@ -448,6 +450,7 @@ void dev_slot_free(DevSlot& d) {
   if (d.d_out) (void)hipFree(d.d_out);
   host_free(d.h_out);
   host_free(d.h_hdr);
+  if (d.copied) (void)hipEventDestroy(d.copied);
   if (d.stream) (void)hipStreamDestroy(d.stream);
   d = DevSlot{};
 }
@@ -775,15 +778,12 @@ constexpr uint64_t kJoinGap = 4096;
 // A registered (pinned) source goes to the device without the staging copy,
 // one H2D per run, when its group's runs average at least kDirectMinRun:
 // below that, per-copy overhead costs more than the host memcpy it saves.
-// And only for a worker's job of at most kDirectMaxJob bytes.  Measured on
-// one MI355X (tools/e2e_sizes.py --register): direct is 15 %
-// faster at 64-256 MiB (no host copy ahead of the first H2D) but 14-15 %
-// slower at 1-4 GiB, because there a group's H2D from registered memory did
-// not start before the previous group's kernel had finished (rocprofv3 trace,
-// profiles/r02/registered_trace/), while the staged pieces overlap the
-// kernels.
+// Measured on one MI355X (tools/e2e_sizes.py --register), with
+// each batch's copies ordered after the previous batch's (worker_run): 14.4
+// against 12.0-12.5 GiB/s staged at 64 MiB, 44.4-45.1 against 29.5-42.8 at
+// 1 GiB, 49.6-50.6 against 33.6-49.5 at 4 GiB.  LBF_DIRECT_MAX_MB (an A/B
+// knob) caps the job size that goes direct; by default every size does.
 constexpr uint64_t kDirectMinRun = 1ull << 20;
-constexpr uint64_t kDirectMaxJob = 512ull << 20;
 
 // Process descriptors [begin, end) on one worker.  They are staged in source
 // order: sorted by offset (a stable permutation, skipped when the table is
@@ -858,10 +858,12 @@ int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
       if (int rc = ensure_dev_slots(w, largest, groups)) return rc;
     }
   }
-  // LBF_DIRECT_MAX_MB: test/A-B knob for the size rule (read per job)
-  const uint64_t direct_max = (uint64_t)env_u64("LBF_DIRECT_MAX_MB", kDirectMaxJob >> 20) << 20;
+  // LBF_DIRECT_MAX_MB: A/B knob, the largest job (per worker) sent direct; unset = no limit
+  const uint64_t direct_max_mb = env_u64("LBF_DIRECT_MAX_MB", 0);
+  const uint64_t direct_max = direct_max_mb ? direct_max_mb << 20 : UINT64_MAX;
   const bool direct_job = job.src.pinned && job_bytes <= direct_max;
   int cur = 0, hcur = 0;
+  int prev_direct = -1;  // device slot of the last direct-route batch
   uint64_t i = begin;
   int rc = LBF_OK;
   long group = 0;
@@ -936,10 +938,20 @@ int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
       uint8_t* h_header = nullptr;
       for (Run& r : runs) r.avail = 0;
       if (direct) {
-        // Runs go as copies of at most 32 MiB (LBF_DIRECT_PIECE_MB, an A/B knob; 0 = one copy per
-        // run): with every group direct, 4 GiB jobs ran at 47.2 GiB/s so against 42.5 as whole
-        // runs, 1 GiB at 39.6 against 35.4 (profiles/r02/registered_trace/piece_sweep/).
-        const uint64_t piece = env_u64("LBF_DIRECT_PIECE_MB", 32) << 20;
+        // A batch's copies start only once the previous direct batch's have
+        // landed.  Issued freely, the copies of every batch in the ring shared
+        // the link, all batches finished copying together, and the link then
+        // sat idle through their kernels (rocprofv3 trace,
+        // profiles/r02/registered_trace/direct_ordered/).  In order, batch g
+        // is hashed while batch g+1 is still copying, as on the staged route.
+        if (prev_direct >= 0 && prev_direct != cur &&
+            !hip_ok(hipStreamWaitEvent(s.stream, w.dev[prev_direct].copied, 0), "hipStreamWaitEvent"))
+          break;
+        // One copy per run (LBF_DIRECT_PIECE_MB, an A/B knob, cuts runs into pieces of that
+        // size).  Before the copies were ordered, 32 MiB pieces helped (4 GiB 42.5 -> 47.2
+        // GiB/s, profiles/r02/registered_trace/piece_sweep/); ordered, whole runs are as fast
+        // or faster (50.6 against 49.6-49.8 GiB/s at 4 GiB, direct_ordered/).
+        const uint64_t piece = env_u64("LBF_DIRECT_PIECE_MB", 0) << 20;
         for (Run& r : runs) {
           const uint64_t step = piece ? piece : r.len;
           for (uint64_t at = 0; at < r.len && rc == LBF_OK; at += step)
@@ -950,6 +962,8 @@ int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
           if (rc) break;
           r.avail = r.len;
         }
+        if (rc || !hip_ok(hipEventRecord(s.copied, s.stream), "hipEventRecord")) break;
+        prev_direct = cur;
       }
       (direct ? w.bytes_direct : w.bytes_staged) += cursor;
       std::vector<bool> cut_short(runs.size(), false);

@@ -555,7 +555,7 @@ int main(int argc, char** argv) {
   const U64 slot = ((U64)o.chunksize + 15) & ~15ull;
   // The arenas live for the whole transfer: pinned once, each batch's verify
   // copies them straight to HBM instead of through the context's staging
-  // (lbf_host_register; batches are far under its 512 MiB direct limit).
+  // (lbf_host_register).
   // Registration pins whole pages, so each arena starts on a page of its own.
   const U64 page = (U64)sysconf(_SC_PAGESIZE);
   const U64 arena_len = slot * o.batch, arena_stride = (arena_len + page - 1) / page * page;

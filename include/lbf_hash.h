@@ -106,11 +106,11 @@ int lbf_verify_batch(lbf_ctx* ctx, const uint8_t* base, uint64_t base_len,
  * straight from it, one H2D per run of adjacent chunks, instead of passing
  * through the context's pinned staging: host DRAM then carries each byte
  * once, not three times (the staging memcpy's read and write, then the DMA
- * read).  Groups of small scattered chunks (runs under 1 MiB on average),
- * and jobs over 512 MiB per device, still go through staging: on one MI355X
- * the direct route is ~15 % faster up to 256 MiB and ~15 % slower from 1 GiB
- * (DESIGN.md §3).  Meant for buffers reused across calls (a peer's receive
- * arenas, a resident file image); registering 4 GiB took ~6 ms.  Memory
+ * read).  Groups of small scattered chunks (runs under 1 MiB on average)
+ * still go through staging.  On one MI355X the direct route ran 14 against
+ * 12 GiB/s at 64 MiB and 50 against 34-50 GiB/s at 4 GiB.
+ * Meant for buffers reused across calls (a peer's receive arenas, a resident
+ * file image); registering 4 GiB took ~6 ms.  Memory
  * that is already pinned is accepted and left pinned.  Pinning is per page:
  * ranges held by one context may not share a page (give each registered
  * buffer pages of its own).  Unregister (with the pointer passed here) before
