@@ -35,6 +35,12 @@ class Oracle:
         lib.oracle_synth_word.restype = _c.c_uint64
         lib.oracle_synth_fill.argtypes = [_c.c_void_p, _c.c_uint64, _c.c_uint64, _c.c_uint64]
         lib.oracle_synth_fill_mt.argtypes = [_c.c_void_p, _c.c_uint64, _c.c_uint64, _c.c_uint64, _c.c_int]
+        # oracle/sha1_unrolled.c: the reference-shaped comparator bench.py times
+        lib.unrolled_sha1.argtypes = [_c.c_void_p, _c.c_uint32, _c.c_void_p]
+        lib.unrolled_sha1_batch.argtypes = [_c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_uint64, _c.c_void_p,
+                                            _c.c_int]
+        lib.unrolled_clock_probe.argtypes = [_c.c_uint64]
+        lib.unrolled_clock_probe.restype = _c.c_uint64
         self.lib = lib
 
     @staticmethod
@@ -84,6 +90,28 @@ class Oracle:
             self.lib.oracle_sha1_batch(self._ptr(base), offs.ctypes.data, szs.ctypes.data, offs.size,
                                        out.ctypes.data, nthreads)
         return out
+
+    def sha1_unrolled(self, data) -> bytes:
+        buf = np.frombuffer(memoryview(data), dtype=np.uint8) if not isinstance(data, np.ndarray) else data
+        out = (_c.c_uint8 * 20)()
+        self.lib.unrolled_sha1(self._ptr(buf), buf.size, out)
+        return bytes(out)
+
+    def sha1_batch_unrolled(self, base: np.ndarray, offsets, sizes, nthreads: int = 1) -> np.ndarray:
+        offs = np.ascontiguousarray(offsets, dtype=np.uint64)
+        szs = np.ascontiguousarray(sizes, dtype=np.uint32)
+        out = np.zeros((offs.size, 20), dtype=np.uint8)
+        if offs.size:
+            self.lib.unrolled_sha1_batch(self._ptr(base), offs.ctypes.data, szs.ctypes.data, offs.size,
+                                         out.ctypes.data, nthreads)
+        return out
+
+    def clock_ghz(self, iters: int = 200_000_000) -> float:
+        """Approximate clock of the calling core (dependent-add chain, one per cycle)."""
+        import time
+        t0 = time.perf_counter()
+        self.lib.unrolled_clock_probe(iters)
+        return iters / (time.perf_counter() - t0) / 1e9
 
     def synth(self, seed: int, start: int, length: int, nthreads: int = 1) -> np.ndarray:
         out = np.empty(length, dtype=np.uint8)

@@ -218,3 +218,41 @@ def test_sha1_batch_property_ragged(oracle, sizes, seed):
     got = oracle.sha1_batch(base, np.array(offs, np.uint64), np.array(sizes, np.uint32))
     for k, (o, s) in enumerate(zip(offs, sizes)):
         assert bytes(got[k]) == hashlib.sha1(base[o:o + s].tobytes()).digest()
+
+
+# --------------------------------------------------------------------------- the timed CPU comparator
+def test_unrolled_comparator_kats_and_hmac(oracle, golden):
+    """oracle/sha1_unrolled.c, the reference-shaped comparator that bench.py's
+    cpu_baseline times, answers the Crypto++ SHA-1 and HMAC(SHA-1) KATs."""
+    for k in golden("kat.json")["kats"]:
+        assert oracle.sha1_unrolled(_kat_message(k)).hex() == k["hex"], k["name"]
+    for name, g, want in hmac_sha1_cases(lambda ms: [oracle.sha1_unrolled(m) for m in ms]):
+        assert g == want, name
+
+
+def test_unrolled_comparator_tails_ragged_c1(oracle, golden):
+    """Same goldens as the checker: the padding tails, the ragged batch (unaligned
+    offsets, threaded) and C1 in full."""
+    for t in golden("synthetic.json")["tails"]:
+        data = oracle.synth(t["seed"], 0, t["size"])
+        n = (t["size"] + t["chunk_size"] - 1) // t["chunk_size"]
+        offs = np.arange(n, dtype=np.uint64) * np.uint64(t["chunk_size"])
+        sizes = np.minimum(t["chunk_size"], t["size"] - offs.astype(np.int64)).astype(np.uint32)
+        got = [oracle.b64_27(bytes(d)) for d in oracle.sha1_batch_unrolled(data, offs, sizes)]
+        assert got == t["b64"], (t["size"], t["chunk_size"])
+    r = golden("synthetic.json")["ragged"]
+    buf = oracle.synth(r["seed"], 0, r["buf_len"])
+    got = oracle.sha1_batch_unrolled(buf, r["offsets"], r["sizes"], nthreads=4)
+    assert [bytes(d).hex() for d in got] == r["hex"]
+    c1 = golden("c1.json")
+    data = oracle.synth(c1["seed"], 0, c1["size"])
+    n = c1["size"] // c1["chunk_size"]
+    offs = np.arange(n, dtype=np.uint64) * np.uint64(c1["chunk_size"])
+    got = oracle.sha1_batch_unrolled(data, offs, np.full(n, c1["chunk_size"], np.uint32), nthreads=3)
+    assert [oracle.b64_27(bytes(d)) for d in got] == c1["b64"]
+
+
+@settings(max_examples=200, deadline=None)
+@given(st.binary(min_size=0, max_size=1200))
+def test_unrolled_comparator_equals_checker(oracle, data):
+    assert oracle.sha1_unrolled(data) == oracle.sha1(data) == hashlib.sha1(data).digest()
