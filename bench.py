@@ -17,8 +17,20 @@ Every rank checks its own digests against the committed golden for its shard
 line, so a multi-GPU run validates itself.
 
 Launch:  python bench.py [--gpus N --steps K --warmup W] [--config c2|c4]
-   N>1:  python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
-Rank 0 prints ONE JSON line.
+   N>1, either way:
+     python bench.py --gpus N ...              (bench.py starts the N rank processes itself)
+     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+   Rank 0 prints ONE JSON line.  The process group is RCCL ("nccl"); with more
+   ranks than visible GPUs (rehearsals on a small box) the self-launch uses gloo
+   and the line says so (LBF_BENCH_BACKEND overrides).
+
+N>1 also measures, after the timed region:
+  * e2e: every rank hashes (the first 4 GiB of) its shard from host memory at
+    the same moment, pageable and then registered, through its own NUMA-local
+    lbf_ctx -- the copy-inclusive rate of north_star at N ranks;
+  * e2e_inprocess: rank 0 alone, after the others have finished, hashes one
+    registered N x 4 GiB host buffer through ONE lbf_ctx over every visible
+    device (Encoder::EncodeFile's shape on an N-GPU node).
 """
 import math
 import argparse
@@ -62,6 +74,8 @@ PCX4_CYCLES_PER_BLOCK = 40 * 23.2 + 40 * 5 * 4.09
 #    byte-swaps words 0..15 since round 2)
 PCX5_CYCLES_PER_BLOCK = 64 * 23.2 + 16 * 5 * 4.09
 FUSED_VALU_PER_BLOCK = 613
+# bytes per rank of the N>1 copy-inclusive leg (the whole C2 shard; C4's first 4 GiB)
+E2E_SLICE_BYTES = 4 * GIB
 
 
 def parse():
@@ -80,21 +94,124 @@ def parse():
     ap.add_argument("--no-e2e", action="store_true", help="skip the host->device->host rate")
     ap.add_argument("--no-other-configs", action="store_true",
                     help="skip the device-resident C3 and C4 measurements that follow the main line at N=1")
+    ap.add_argument("--no-inproc", action="store_true",
+                    help="N>1: skip the single-process all-device host-memory leg (e2e_inprocess)")
     a = ap.parse_args()
     a.chunk_size = a.chunk_size or {"c2": 262144, "c4": 1 << 20}[a.config]
     a.file_gib = a.file_gib or {"c2": 4.0, "c4": 32.0}[a.config]
     return a
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def rank_env(base, n, port, backend=None):
+    """The environment of each of n self-launched ranks: what torch.distributed.run
+    would export (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_*), one node."""
+    common = dict(base, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(n),
+                  LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", LBF_BENCH_LAUNCHER="bench.py")
+    if backend:
+        common["LBF_BENCH_BACKEND"] = backend
+    return [dict(common, RANK=str(r), LOCAL_RANK=str(r)) for r in range(n)]
+
+
+def spawn_ranks(n, argv, script=None, python=None, env=None, grace_s=15.0):
+    """`bench.py --gpus N` without a launcher: start N fresh rank processes of
+    this script and wait for them.  The parent makes no GPU call (importing
+    torch and counting devices do not initialise HIP on this image) and never
+    execs: the ranks are children.  Rank 0 inherits stdout and prints the one
+    JSON line; the other ranks' stdout goes to stderr.  If a rank fails, the
+    others are stopped (by PID) and its exit status is returned."""
+    import signal
+    import subprocess
+    base = dict(os.environ if env is None else env)
+    backend = None
+    if "LBF_BENCH_BACKEND" not in base:
+        ndev = torch.cuda.device_count()
+        if ndev < n:
+            # RCCL refuses two ranks on one device: a rehearsal on a small box
+            backend = "gloo"
+            print(f"bench.py: {n} ranks on {ndev} visible GPU(s): process group gloo (rehearsal)", file=sys.stderr)
+    envs = rank_env(base, n, _free_port(), backend)
+    cmd = [python or sys.executable, script or os.path.abspath(__file__)] + list(argv)
+    procs = []
+    try:
+        for r in range(n):
+            procs.append(subprocess.Popen(cmd, env=envs[r], stdout=subprocess.PIPE if r == 0 else sys.stderr))
+    except BaseException:
+        for p in procs:
+            p.kill()
+        raise
+
+    def relay(pipe):
+        # rank 0's JSON line to stdout; anything else it prints (gloo's C++
+        # connection notice goes to stdout) to stderr, so stdout stays one line
+        for raw in iter(pipe.readline, b""):
+            line = raw.decode(errors="replace")
+            dst = sys.stdout if line.lstrip().startswith("{") else sys.stderr
+            dst.write(line)
+            dst.flush()
+
+    import threading
+    relay_t = threading.Thread(target=relay, args=(procs[0].stdout,), daemon=True)
+    relay_t.start()
+
+    def stop_all(*_):
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+
+    old = signal.signal(signal.SIGTERM, lambda *a: (stop_all(), sys.exit(143)))
+    rc = 0
+    try:
+        live = list(procs)
+        while live:
+            for p in list(live):
+                c = p.poll()
+                if c is None:
+                    continue
+                live.remove(p)
+                if c != 0 and rc == 0:
+                    rc = c if c > 0 else 128 - c
+                    print(f"bench.py: rank {procs.index(p)} exited with {c}; stopping the others", file=sys.stderr)
+                    stop_all()
+                    deadline = time.time() + grace_s
+                    for q in live:
+                        try:
+                            q.wait(timeout=max(0.1, deadline - time.time()))
+                        except subprocess.TimeoutExpired:
+                            q.kill()
+            time.sleep(0.1)
+    finally:
+        signal.signal(signal.SIGTERM, old)
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+        relay_t.join(timeout=10)
+    return rc
+
+
 def dist_setup(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world:
+        # only reachable under an outside launcher whose world differs from --gpus:
+        # refuse rather than print a line whose n_gpus is not what was asked for
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher's WORLD_SIZE is {world}")
+    ndev = max(1, torch.cuda.device_count())
+    # one rank per GPU; more ranks than GPUs only for rehearsals of the
+    # multi-rank flow on a small box (process group gloo)
+    dev = local % ndev
     if world > 1:
         import torch.distributed as dist
-        # one rank per GPU; more ranks than GPUs only for rehearsals of the
-        # multi-rank flow on a small box (LBF_BENCH_BACKEND=gloo)
-        dev = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(dev)
         backend = os.environ.get("LBF_BENCH_BACKEND", "nccl")
         if backend == "nccl":
@@ -103,10 +220,7 @@ def dist_setup(args):
             dist.init_process_group(backend, rank=rank, world_size=world)
     else:
         torch.cuda.set_device(0)
-    if args.gpus != world:
-        if rank == 0:
-            print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using {world}", file=sys.stderr)
-    return rank, world, local
+    return rank, world, local, dev, ndev
 
 
 def barrier(world):
@@ -164,12 +278,16 @@ def host_cpus():
 
 
 def cpu_baseline(args, stream_start, n_chunks_sample, gpu_digests_sample):
-    """The oracle restatement of the reference encoder hash (portable C -O2,
-    oracle/sha1_oracle.c) on the host cores, over a bounded sample of the same
-    synthetic bytes.  kind="port": building the reference was denied
-    (SURVEY.md §8c).  Threads: every CPU the process may use (SURVEY.md §8d
-    (ii)), i.e. its affinity mask capped by the cgroup CPU quota; the same
-    sample on one thread per affinity CPU shows what the quota allows."""
+    """The reference encoder's hash on the host cores, over a bounded sample of
+    the same synthetic bytes.  `value` times oracle/sha1_unrolled.c: portable C
+    -O2 in the shape of the reference's Crypto++ 5.2.1 Transform (80 unrolled
+    rounds, rolling W[i&15]; sha.cpp:34-69), the speed the reference itself
+    compiles to.  kind="port": building the reference was denied (SURVEY.md
+    §8c).  The checker oracle's loop form (oracle/sha1_oracle.c, ~1.5x slower)
+    is kept as `loop_form`.  Threads: every CPU the process may use (SURVEY.md
+    §8d (ii)), i.e. its affinity mask capped by the cgroup CPU quota; the
+    reference encoder itself is one thread (Encoder.cpp:40-79), timed as
+    `single_thread_value`."""
     from tests.oracle_lib import Oracle
     orc = Oracle()
     cs = args.chunk_size
@@ -179,52 +297,62 @@ def cpu_baseline(args, stream_start, n_chunks_sample, gpu_digests_sample):
     data = orc.synth(SEED_C, stream_start, nbytes, nthreads=threads)
     offs = np.arange(n_chunks_sample, dtype=np.uint64) * np.uint64(cs)
     sizes = np.full(n_chunks_sample, cs, dtype=np.uint32)
+    clock0 = orc.clock_ghz()
 
-    def rate(nthreads, min_s=3.0, max_reps=20):
+    def rate(fn, nthreads, n=n_chunks_sample, min_s=3.0, max_reps=20):
         reps, t = 0, 0.0
         d = None
         while t < min_s and reps < max_reps:
             t0 = time.perf_counter()
-            d = orc.sha1_batch(data, offs, sizes, nthreads=nthreads)
+            d = fn(data, offs[:n], sizes[:n], nthreads=nthreads)
             t += time.perf_counter() - t0
             reps += 1
-        return reps * nbytes / GIB / t, reps, d
+        return reps * n * cs / GIB / t, reps, d
 
     # all usable host cores, chunk-parallel
-    mt_gibs, reps, d_mt = rate(threads)
+    mt_gibs, reps, d_mt = rate(orc.sha1_batch_unrolled, threads)
     # one thread per CPU of the affinity mask (256 on a GPU box): what the quota lets through
-    aff_gibs = rate(affinity, min_s=1.0, max_reps=3)[0] if affinity != threads else mt_gibs
-    # one thread, like Encoder.cpp:40-79 (bounded to 1/4 of the sample)
+    aff_gibs = rate(orc.sha1_batch_unrolled, affinity, min_s=1.0, max_reps=3)[0] if affinity != threads else mt_gibs
+    # one thread, like Encoder.cpp:40-79 (a quarter of the sample)
     n1 = max(1, n_chunks_sample // 4)
-    t0 = time.perf_counter()
-    d_1 = orc.sha1_batch(data, offs[:n1], sizes[:n1], nthreads=1)
-    t_1 = time.perf_counter() - t0
-    st_gibs = n1 * cs / GIB / t_1
+    st_gibs, _, d_1 = rate(orc.sha1_batch_unrolled, 1, n=n1, min_s=0.0, max_reps=1)
+    clock1 = orc.clock_ghz()
+    # the checker's loop form, for continuity with round 1-2 lines
+    loop_mt = rate(orc.sha1_batch, threads, min_s=1.5, max_reps=10)
+    loop_st = rate(orc.sha1_batch, 1, n=n1 // 2 or 1, min_s=0.0, max_reps=1)
     # fread-inclusive single-thread encode of the same bytes as a file, as
-    # Encoder::EncodeFile does it (one chunk buffer, fread + hash per chunk;
-    # oracle_encode_file); the file is page-cache warm, written just before
+    # Encoder::EncodeFile does it (one chunk buffer, fread + hash per chunk);
+    # the file is page-cache warm, written just before
     import tempfile
     fread = None
     with tempfile.NamedTemporaryFile(prefix="lbf_cpu_sample_", dir=os.environ.get("TMPDIR", "/tmp")) as f:
         data[: n1 * cs].tofile(f.name)
         dig = np.zeros((n1, 20), dtype=np.uint8)
         t0 = time.perf_counter()
-        got = orc.lib.oracle_encode_file(f.name.encode(), cs, dig.ctypes.data, n1, None)
+        got = orc.lib.unrolled_encode_file(f.name.encode(), cs, dig.ctypes.data, n1)
         t_f = time.perf_counter() - t0
         if got == n1:
             fread = {"value": round(n1 * cs / GIB / t_f, 3), "unit": "GiB/s",
                      "sample": f"{n1} x {cs // 1024} KiB chunks from a page-cached file, 1 thread",
                      "parity_vs_gpu": bool(np.array_equal(dig, gpu_digests_sample[:n1]))}
-    parity = bool(np.array_equal(d_mt, gpu_digests_sample) and np.array_equal(d_1, gpu_digests_sample[:n1]))
+    parity = bool(np.array_equal(d_mt, gpu_digests_sample) and np.array_equal(d_1, gpu_digests_sample[:n1])
+                  and np.array_equal(loop_mt[2], gpu_digests_sample))
     return {
         "value": round(mt_gibs, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+        "implementation": "oracle/sha1_unrolled.c: unrolled 80-round Transform in Crypto++ 5.2.1's shape "
+                          "(sha.cpp:34-69), gcc -O2, portable C, no SHA-NI",
         "sample": f"{n_chunks_sample} x {cs // 1024} KiB chunks ({nbytes / GIB:.2f} GiB) of the same stream, "
                   f"{reps} pass(es) on {threads} threads; single-thread pass over {n1} chunks",
         "single_thread_value": round(st_gibs, 3),
         "affinity_threads_value": round(aff_gibs, 3),
         "single_thread_fread_encode": fread,
+        "loop_form": {"value": round(loop_mt[0], 3), "single_thread_value": round(loop_st[0], 3),
+                      "implementation": "oracle/sha1_oracle.c (the parity checker: rounds as a loop)"},
         "host": {**_host_desc(), "affinity_cores": affinity, "cgroup_cpu_quota": quota, "usable_cores": usable,
-                 "numa_nodes": _numa_nodes()},
+                 "numa_nodes": _numa_nodes(),
+                 "clock_ghz_measured": [round(clock0, 3), round(clock1, 3)],
+                 "clock_note": "one core, dependent-add chain (oracle unrolled_clock_probe), before and after "
+                               "the multi-thread passes"},
         "parity_vs_gpu": parity,
     }, data
 
@@ -238,7 +366,13 @@ def _host_desc():
                 break
     except Exception:
         pass
-    return {"cpu_model": model, "os_cpu_count": os.cpu_count()}
+    out = {"cpu_model": model, "os_cpu_count": os.cpu_count()}
+    try:
+        khz = int(open("/sys/devices/system/cpu/cpu0/cpufreq/cpuinfo_max_freq").read())
+        out["cpufreq_max_ghz"] = round(khz / 1e6, 3)
+    except Exception:
+        pass
+    return out
 
 
 def compute_floor_ms(variant, cs, n_chunks):
@@ -258,42 +392,109 @@ def compute_floor_ms(variant, cs, n_chunks):
     return max(chain, chip) * 1e3
 
 
-def e2e_rate(host_data, cs):
-    """Host bytes in -> host digests out through the lbf_ctx pinned pipeline
-    (PCIe-inclusive rate for DESIGN.md; never the headline value), from
-    pageable memory and from the same memory registered with the context."""
+def e2e_leg(host_data, cs, dev, world):
+    """Host bytes in -> host digests out through this rank's lbf_ctx (pinned,
+    NUMA-local staging on its GPU), from pageable memory and then from the same
+    memory registered with the context (lbf_host_register: straight to HBM, no
+    staging memcpy).  The PCIe-inclusive rate of north_star; never `value`.
+
+    With world > 1 every rank runs each pass at the same moment (a barrier
+    before each), so the aggregate world x bytes / slowest rank is what N GPUs
+    pull over their links and host DRAM together.  Best of 3 passes per route,
+    after one untimed pass that sizes the context's pinned staging."""
     from bitflood_amd import ChunkHasher, chunk_table
     offs, sizes = chunk_table(host_data.size, cs)
-    with ChunkHasher(device_mask=1) as h:
-        # warm: one untimed pass sizes the context's pinned staging to this job
-        # (it grows on demand; tools/file_rate.py reports the one-shot cost)
-        h.hash_chunks(host_data, offs, sizes)
-        t = float("inf")
-        for _ in range(3):  # best of 3: a lone pass swings with the host's other tenants
+    gib = host_data.size / GIB
+
+    def passes(h, k=3):
+        best_agg, best_own, d = 0.0, float("inf"), None
+        for _ in range(k):
+            barrier(world)
             t0 = time.perf_counter()
             d = h.hash_chunks(host_data, offs, sizes)
-            t = min(t, time.perf_counter() - t0)
+            t = time.perf_counter() - t0
+            t_max = max_over_ranks(t, world)
+            best_agg = max(best_agg, world * gib / t_max)
+            best_own = min(best_own, t)
+        return best_agg, gib / best_own, d
+
+    with ChunkHasher(device_mask=1 << dev) as h:
+        h.hash_chunks(host_data, offs, sizes)  # warm: sizes the staging to this job
+        pag_agg, pag_own, d_pag = passes(h)
         placement = h.worker_info(0)
-        # The same bytes from caller memory registered with the context
-        # (lbf_host_register): straight to HBM with ordered copies, no staging
-        # memcpy.  Pinning is a one-off cost of a reused buffer, reported apart.
         t0 = time.perf_counter()
         h.register_host(host_data)
         reg_s = time.perf_counter() - t0
         s0 = h.staging_stats()
-        t_reg = float("inf")
         try:
-            for _ in range(3):
-                t0 = time.perf_counter()
-                d_reg = h.hash_chunks(host_data, offs, sizes)
-                t_reg = min(t_reg, time.perf_counter() - t0)
+            reg_agg, reg_own, d_reg = passes(h)
             s1 = h.staging_stats()
         finally:
             h.unregister_host(host_data)
-    registered = {"gibs": round(host_data.size / GIB / t_reg, 3), "register_s": round(reg_s, 4),
-                  "direct_fraction": round((s1["direct"] - s0["direct"]) / max(1, 3 * host_data.size), 4),
-                  "parity": bool(np.array_equal(d_reg, d))}
-    return host_data.size / GIB / t, d, placement, registered
+    return {"pageable_agg": pag_agg, "pageable_own": pag_own, "registered_agg": reg_agg,
+            "registered_own": reg_own, "register_s": reg_s,
+            "direct_fraction": (s1["direct"] - s0["direct"]) / max(1, 3 * host_data.size),
+            "digests": d_pag, "registered_equal": bool(np.array_equal(d_reg, d_pag)), "placement": placement}
+
+
+def inproc_leg(buf, slice_bytes, cs, shard_starts, slice_hashes):
+    """EncodeFile's shape on an N-GPU node: ONE process, ONE lbf_ctx over every
+    visible device, lbf_sha1_batch on one N x slice_bytes host buffer (slice r
+    = the bytes rank r hashed in its e2e leg), registered, then pageable.  Run
+    by rank 0 after the other ranks have finished.  `buf` (a device buffer of
+    at least slice_bytes) generates each slice; parity: slice r's digests must
+    hash to rank r's reported slice hash (its device-resident digests, which
+    were checked against the golden of its shard)."""
+    from bitflood_amd import ChunkHasher, chunk_table
+    world = len(shard_starts)
+    total = world * slice_bytes
+    big = np.empty(total, dtype=np.uint8)
+    for r, start in enumerate(shard_starts):
+        buf.fill_synthetic(SEED_C, start=start, nbytes=slice_bytes)
+        H.synchronize()
+        buf.download_into(big[r * slice_bytes:(r + 1) * slice_bytes])
+    offs, sizes = chunk_table(total, cs)
+    per_slice = slice_bytes // cs
+    gib = total / GIB
+
+    def best(h, k):
+        t, d = float("inf"), None
+        for _ in range(k):
+            t0 = time.perf_counter()
+            d = h.hash_chunks(big, offs, sizes)
+            t = min(t, time.perf_counter() - t0)
+        return gib / t, d
+
+    with ChunkHasher(device_mask=0) as h:
+        info = [h.worker_info(w) for w in range(h.num_workers)]
+        ndev = h.num_devices
+        h.hash_chunks(big, offs, sizes)  # warm: every worker's staging and device slots
+        pag, d_pag = best(h, 2)
+        t0 = time.perf_counter()
+        h.register_host(big)
+        reg_s = time.perf_counter() - t0
+        try:
+            reg, d_reg = best(h, 3)
+            st = h.staging_stats()
+        finally:
+            h.unregister_host(big)
+    del big
+    ok = [int(slice_hash(d_reg[r * per_slice:(r + 1) * per_slice]) == slice_hashes[r]) for r in range(world)]
+    return {
+        "what": "one process, one lbf_ctx over every visible device, lbf_sha1_batch on one host buffer of "
+                f"{world} x {slice_bytes / GIB:g} GiB (slice r = rank r's e2e bytes)",
+        "devices": ndev, "workers": len(info), "workers_per_device": int(os.environ.get("LBF_WORKERS_PER_DEVICE", "1")),
+        "bytes": total, "chunk_size": cs,
+        "registered_gibs": round(reg, 3), "register_s": round(reg_s, 4), "pageable_gibs": round(pag, 3),
+        "direct_bytes": st["direct"],
+        "parity_per_slice": ok, "parity": all(ok) and bool(np.array_equal(d_reg, d_pag)),
+        "placement": info,
+    }
+
+
+def slice_hash(digests):
+    """56-bit fingerprint of a digest slice (fits an int64 all-gather)."""
+    return int.from_bytes(hashlib.sha1(np.ascontiguousarray(digests).tobytes()).digest()[:7], "big")
 
 
 def golden_for_rank(args, rank, file_bytes):
@@ -387,21 +588,32 @@ def other_configs():
     return res
 
 
-def gather_ints(x, world):
+def _gather(x, world, dtype):
     if world == 1:
-        return [int(x)]
+        return [x]
     import torch.distributed as dist
     backend = dist.get_backend()
     dev = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
-    t = torch.tensor([int(x)], dtype=torch.int64, device=dev)
+    t = torch.tensor([x], dtype=dtype, device=dev)
     parts = [torch.empty_like(t) for _ in range(world)]
     dist.all_gather(parts, t)
-    return [int(p.item()) for p in parts]
+    return [p.item() for p in parts]
+
+
+def gather_ints(x, world):
+    return [int(v) for v in _gather(int(x), world, torch.int64)]
+
+
+def gather_floats(x, world):
+    return [float(v) for v in _gather(float(x), world, torch.float64)]
 
 
 def main():
     args = parse()
-    rank, world, local = dist_setup(args)
+    if args.gpus > 1 and "RANK" not in os.environ:
+        # no outside launcher: start the N ranks here (children, never exec)
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
+    rank, world, local, dev, ndev = dist_setup(args)
     if args.variant:
         H.set_kernel_variant(args.variant)
     cs = args.chunk_size
@@ -441,6 +653,7 @@ def main():
     ev_ms = e0.elapsed_time(e1)
     t_max = max_over_ranks(wall, world)
     ev_max = max_over_ranks(ev_ms, world)
+    per_rank_kernel_ms = [round(x / args.steps, 4) for x in gather_floats(ev_ms, world)]
 
     total_bytes = world * file_bytes * args.steps
     value = total_bytes / GIB / t_max
@@ -451,6 +664,38 @@ def main():
     # every rank checks its own shard against the committed golden
     gold, gold_path = golden_for_rank(args, rank, file_bytes)
     per_rank = gather_ints(check_golden(gold, digests), world)
+    per_rank_dev = gather_ints(dev, world)
+
+    # N>1: the copy-inclusive rate with every rank pulling from host memory at once
+    e2e_multi = None
+    slice_bytes = min(file_bytes, E2E_SLICE_BYTES)
+    n_slice = slice_bytes // cs
+    if world > 1 and not args.no_e2e:
+        host = buf.download(slice_bytes)
+        r = e2e_leg(host, cs, dev, world)
+        del host
+        ok = int(np.array_equal(r["digests"], digests[:n_slice]) and r["registered_equal"])
+        g = {k: gather_floats(r[k], world) for k in ("pageable_own", "registered_own", "register_s")}
+        e2e_multi = {
+            "what": f"every rank hashes the first {slice_bytes / GIB:g} GiB of its shard from host memory at the "
+                    "same moment through its own lbf_ctx (NUMA-local pinned staging), pageable then registered; "
+                    "best of 3 synchronized passes",
+            "bytes_per_rank": slice_bytes, "chunk_size": cs,
+            "pageable": {"aggregate_gibs": round(r["pageable_agg"], 3),
+                         "per_rank_gibs": [round(x, 3) for x in g["pageable_own"]]},
+            "registered": {"aggregate_gibs": round(r["registered_agg"], 3),
+                           "per_rank_gibs": [round(x, 3) for x in g["registered_own"]],
+                           "register_s_per_rank": [round(x, 4) for x in g["register_s"]],
+                           "direct_fraction_rank0": round(r["direct_fraction"], 4)},
+            "parity_per_rank": gather_ints(ok, world),
+            "numa_per_rank": [{"device": d, "numa_node": n, "staging_node": s} for d, n, s in zip(
+                per_rank_dev, gather_ints(r["placement"]["numa_node"], world),
+                gather_ints(r["placement"]["staging_node"], world))],
+        }
+        e2e_multi["parity"] = all(x == 1 for x in e2e_multi["parity_per_rank"])
+    slice_hashes = gather_ints(slice_hash(digests[:n_slice]), world)
+    shard_starts = [shard_range(world * n_chunks, q, world)[0] * cs for q in range(world)]
+
     variant = H.load().lbf_kernel_for(n_chunks)
     floor_ms = compute_floor_ms(variant, cs, n_chunks)
     kernel = KERNELS.get(variant, str(variant))
@@ -519,7 +764,20 @@ def main():
                 "per_rank": per_rank,  # 1 match, 0 mismatch, -1 no golden for that shard
                 "all_ranks_match_golden": all(x == 1 for x in per_rank),
             },
+            "ranks": {
+                "launcher": os.environ.get("LBF_BENCH_LAUNCHER", "torch.distributed.run" if world > 1 else "none"),
+                "process_group": os.environ.get("LBF_BENCH_BACKEND", "nccl") if world > 1 else None,
+                "visible_gpus": ndev,
+                "device_per_rank": per_rank_dev,
+                "kernel_ms_per_rank": per_rank_kernel_ms,
+                "rehearsal": world > ndev,
+            },
         }
+        if world > ndev:
+            out["ranks"]["note"] = (f"{world} ranks share {ndev} GPU(s): a rehearsal of the N-rank flow; their "
+                                    "launches queue on the shared device, so value is not an N-GPU rate")
+        if e2e_multi is not None:
+            out["e2e"] = e2e_multi
         if world == 1 and not args.no_cpu_baseline:
             sample = min(n_chunks, max(1, GIB // cs))
             cb, host = cpu_baseline(args, stream_start, sample, digests[:sample])
@@ -527,22 +785,30 @@ def main():
             if not args.no_e2e:
                 # the whole file, copied back from HBM into pageable host memory
                 host_file = buf.download(file_bytes)
-                rate, d_e2e, placement, registered = e2e_rate(host_file, cs)
+                r = e2e_leg(host_file, cs, dev, 1)
                 del host_file
-                out["e2e_host_to_host_gibs"] = round(rate, 3)
+                out["e2e_host_to_host_gibs"] = round(r["pageable_own"], 3)
                 out["e2e_bytes"] = file_bytes
-                out["e2e_parity"] = bool(np.array_equal(d_e2e, digests))
-                out["e2e_staging"] = placement
-                out["e2e_registered"] = registered
-                cb["host"]["gpu0_numa_node"] = placement["numa_node"]
+                out["e2e_parity"] = bool(np.array_equal(r["digests"], digests))
+                out["e2e_staging"] = r["placement"]
+                out["e2e_registered"] = {"gibs": round(r["registered_own"], 3), "register_s": round(r["register_s"], 4),
+                                         "direct_fraction": round(r["direct_fraction"], 4),
+                                         "parity": r["registered_equal"]}
+                cb["host"]["gpu0_numa_node"] = r["placement"]["numa_node"]
         out["first_chunk_b64"] = b64_27(bytes(digests[0]))
+    if world > 1:
+        import torch.distributed as dist
+        barrier(world)  # every rank's e2e leg has ended before rank 0 goes on alone
+        dist.destroy_process_group()
+    if rank == 0 and world > 1 and not args.no_e2e and not args.no_inproc:
+        try:
+            out["e2e_inprocess"] = inproc_leg(buf, slice_bytes, cs, shard_starts, slice_hashes)
+        except Exception as e:  # recorded in the line; the main measurement stands
+            out["e2e_inprocess"] = {"error": f"{type(e).__name__}: {e}"}
     buf.free()
     dig.free()
     if rank == 0 and world == 1 and not args.no_other_configs and args.config == "c2":
         out["other_configs"] = other_configs()
-    if world > 1:
-        import torch.distributed as dist
-        dist.destroy_process_group()
     if rank == 0:
         print(json.dumps(out), flush=True)
 

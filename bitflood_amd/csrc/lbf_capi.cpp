@@ -16,6 +16,7 @@
 #include <pthread.h>
 #include <sched.h>
 #include <string.h>
+#include <sys/resource.h>
 #include <sys/syscall.h>
 #include <unistd.h>
 
@@ -23,6 +24,7 @@
 #include <atomic>
 #include <cctype>
 #include <condition_variable>
+#include <cerrno>
 #include <cstdio>
 #include <cstdlib>
 #include <iterator>
@@ -399,7 +401,7 @@ struct Registered {
 struct lbf_ctx {
   std::vector<Worker> workers;
   std::vector<Registered> regs;  // guarded by mu, like every job
-  std::mutex mu;
+  mutable std::mutex mu;
 };
 
 namespace {
@@ -1205,6 +1207,8 @@ extern "C" int lbf_ctx_create(uint32_t device_mask, lbf_ctx** out) {
 extern "C" int lbf_ctx_worker_info(const lbf_ctx* ctx, int worker, int* device, int* numa_node, int* staging_node,
                                    int* bound_cpus) {
   if (!ctx || worker < 0 || worker >= (int)ctx->workers.size()) return fail(LBF_ERR_INVALID, "no such worker");
+  // a running job may grow or trim the slots read below: wait for it
+  std::lock_guard<std::mutex> lock(ctx->mu);
   const Worker& w = ctx->workers[worker];
   if (device) *device = w.device;
   if (numa_node) *numa_node = w.numa_node;
@@ -1273,12 +1277,26 @@ extern "C" int lbf_host_register(lbf_ctx* ctx, const void* ptr, uint64_t len) {
                           (next != g_pins.begin() && std::prev(next)->second.hi > r.lo);
     if (overlaps)
       return fail(LBF_ERR_INVALID, "lbf_host_register: range overlaps, but differs from, one another context holds");
-    hipPointerAttribute_t attr{};
-    if (hipPointerGetAttributes(&attr, reinterpret_cast<void*>(r.lo)) == hipSuccess && attr.type == hipMemoryTypeHost) {
-      ctx->regs.push_back(r);  // pinned already by someone else: use it, never unpin it
+    // Pinned already by someone else (a hipHostMalloc'd buffer, a caller's own
+    // registration): use it, never unpin it -- but only if the whole range is:
+    // both its first and its last page.  The first page alone may belong to a
+    // neighbouring pinned allocation.
+    auto pinned_page = [](uintptr_t p) {
+      hipPointerAttribute_t attr{};
+      const bool yes = hipPointerGetAttributes(&attr, reinterpret_cast<void*>(p)) == hipSuccess &&
+                       attr.type == hipMemoryTypeHost;
+      (void)hipGetLastError();  // pageable memory is an error to that query
+      return yes;
+    };
+    const bool first_pinned = pinned_page(r.lo), last_pinned = pinned_page(r.hi - page);
+    if (first_pinned && last_pinned) {
+      ctx->regs.push_back(r);
       return (int)LBF_OK;
     }
-    (void)hipGetLastError();  // pageable memory is an error to that query
+    if (first_pinned || last_pinned)
+      return fail(LBF_ERR_INVALID,
+                  "lbf_host_register: range is partly pinned already (its first or last page belongs to another "
+                  "pinned allocation)");
     KeepCurrentDevice keep;
     LBF_HIP_TRY(hipSetDevice(ctx->workers[0].device));
     const hipError_t e = hipHostRegister(reinterpret_cast<void*>(r.lo), r.hi - r.lo, hipHostRegisterPortable);
@@ -1344,15 +1362,24 @@ extern "C" int lbf_verify_batch(lbf_ctx* ctx, const uint8_t* base, uint64_t base
   return guarded([&] { return run_job(ctx, job, n); });
 }
 
-extern "C" int lbf_files_ranges(lbf_ctx* ctx, const char* const* paths, uint32_t n_files, const uint32_t* file_of,
-                                const uint64_t* offsets, const uint32_t* sizes, uint64_t n, const uint8_t* expected,
-                                uint8_t* out) {
-  if (!ctx || !paths || n_files == 0) return fail(LBF_ERR_INVALID, "null context/paths or no file");
-  if (n == 0) return LBF_OK;
-  if (!offsets || !sizes || !out || (n_files > 1 && !file_of)) return fail(LBF_ERR_INVALID, "null argument");
-  if (file_of)
-    for (uint64_t i = 0; i < n; ++i)
-      if (file_of[i] >= n_files) return fail(LBF_ERR_INVALID, "chunk " + std::to_string(i) + " names no file");
+namespace {
+
+// Files one job holds open at once: a quarter of the soft RLIMIT_NOFILE, so a
+// caller with sockets and other descriptors still has room (EncodeFile opens
+// one file at a time in the reference, Encoder.cpp:40-79); LBF_FILES_WINDOW
+// overrides.  A flood with more files runs as one job per window of files.
+uint32_t files_window() {
+  if (uint64_t w = env_u64("LBF_FILES_WINDOW", 0)) return (uint32_t)std::min<uint64_t>(w, 1u << 20);
+  rlimit rl{};
+  uint64_t soft = 1024;
+  if (getrlimit(RLIMIT_NOFILE, &rl) == 0 && rl.rlim_cur != RLIM_INFINITY) soft = rl.rlim_cur;
+  return (uint32_t)std::max<uint64_t>(4, std::min<uint64_t>(4096, soft / 4));
+}
+
+// One job over files [0, n_files) of `paths`, all opened up front.
+int files_ranges_job(lbf_ctx* ctx, const char* const* paths, uint32_t n_files, const uint32_t* file_of,
+                     const uint64_t* offsets, const uint32_t* sizes, uint64_t n, const uint8_t* expected,
+                     uint8_t* out) {
   Job job{};
   job.src.fds.assign(n_files, -1);
   struct Closer {  // every opened file is closed on every path
@@ -1363,11 +1390,17 @@ extern "C" int lbf_files_ranges(lbf_ctx* ctx, const char* const* paths, uint32_t
     }
   } closer{job.src.fds};
   for (uint32_t f = 0; f < n_files; ++f) {
-    if (!paths[f]) return fail(LBF_ERR_INVALID, "null path");
     const int fd = open(paths[f], O_RDONLY | O_CLOEXEC);
-    // hash mode needs every file; verify mode leaves a missing file's chunks
-    // '0' (Flood.cpp:257)
-    if (fd < 0 && !expected) return fail(LBF_ERR_IO, std::string("cannot open ") + paths[f]);
+    if (fd < 0) {
+      // Out of descriptors is this process's state, not the file's: an error
+      // in both modes, never verdict 0 (which would queue the chunks for
+      // re-download and overwrite).
+      if (errno == EMFILE || errno == ENFILE)
+        return fail(LBF_ERR_IO, std::string("cannot open ") + paths[f] + ": too many open files");
+      // hash mode needs every file; verify mode leaves a missing file's chunks
+      // '0' (Flood.cpp:257)
+      if (!expected) return fail(LBF_ERR_IO, std::string("cannot open ") + paths[f]);
+    }
     if (fd >= 0) posix_fadvise(fd, 0, 0, POSIX_FADV_SEQUENTIAL);
     job.src.fds[f] = fd;
   }
@@ -1381,7 +1414,59 @@ extern "C" int lbf_files_ranges(lbf_ctx* ctx, const char* const* paths, uint32_t
   job.expected = expected;
   if (expected) job.verdicts = out;
   else job.digests = out;
-  return guarded([&] { return run_job(ctx, job, n); });
+  return run_job(ctx, job, n);
+}
+
+}  // namespace
+
+extern "C" int lbf_files_ranges(lbf_ctx* ctx, const char* const* paths, uint32_t n_files, const uint32_t* file_of,
+                                const uint64_t* offsets, const uint32_t* sizes, uint64_t n, const uint8_t* expected,
+                                uint8_t* out) {
+  if (!ctx || !paths || n_files == 0) return fail(LBF_ERR_INVALID, "null context/paths or no file");
+  if (n == 0) return LBF_OK;
+  if (!offsets || !sizes || !out || (n_files > 1 && !file_of)) return fail(LBF_ERR_INVALID, "null argument");
+  if (file_of)
+    for (uint64_t i = 0; i < n; ++i)
+      if (file_of[i] >= n_files) return fail(LBF_ERR_INVALID, "chunk " + std::to_string(i) + " names no file");
+  for (uint32_t f = 0; f < n_files; ++f)
+    if (!paths[f]) return fail(LBF_ERR_INVALID, "null path");
+  const uint32_t window = files_window();
+  if (n_files <= window || !file_of)
+    return guarded([&] { return files_ranges_job(ctx, paths, n_files, file_of, offsets, sizes, n, expected, out); });
+  // More files than may be open at once: one job per window of `window`
+  // consecutive files, each over that window's chunks (gathered, then the
+  // results scattered back to the caller's indices).
+  return guarded([&]() -> int {
+    const uint32_t n_win = (n_files + window - 1) / window;
+    std::vector<std::vector<uint64_t>> members(n_win);
+    for (uint64_t i = 0; i < n; ++i) members[file_of[i] / window].push_back(i);
+    const size_t per = expected ? 1 : 20;
+    std::vector<uint32_t> fo;
+    std::vector<uint64_t> offs;
+    std::vector<uint32_t> szs;
+    std::vector<uint8_t> exp, res;
+    for (uint32_t w = 0; w < n_win; ++w) {
+      const std::vector<uint64_t>& idx = members[w];
+      if (idx.empty()) continue;
+      const uint32_t f0 = w * window, nf = std::min(window, n_files - f0);
+      fo.resize(idx.size());
+      offs.resize(idx.size());
+      szs.resize(idx.size());
+      res.assign(idx.size() * per, 0);
+      if (expected) exp.resize(idx.size() * 20);
+      for (size_t k = 0; k < idx.size(); ++k) {
+        fo[k] = file_of[idx[k]] - f0;
+        offs[k] = offsets[idx[k]];
+        szs[k] = sizes[idx[k]];
+        if (expected) memcpy(&exp[20 * k], expected + 20 * idx[k], 20);
+      }
+      if (int rc = files_ranges_job(ctx, paths + f0, nf, fo.data(), offs.data(), szs.data(), idx.size(),
+                                    expected ? exp.data() : nullptr, res.data()))
+        return rc;
+      for (size_t k = 0; k < idx.size(); ++k) memcpy(out + per * idx[k], &res[per * k], per);
+    }
+    return LBF_OK;
+  });
 }
 
 extern "C" int lbf_file_ranges(lbf_ctx* ctx, const char* path, const uint64_t* offsets, const uint32_t* sizes,

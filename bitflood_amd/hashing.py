@@ -278,6 +278,15 @@ class DeviceBuffer:
         check(load().lbf_memcpy_d2h(out.ctypes.data, self.ptr + offset, nbytes))
         return out.view(dtype)
 
+    def download_into(self, out: np.ndarray, offset: int = 0) -> None:
+        """Copy out.nbytes bytes from this buffer at `offset` into the existing
+        C-contiguous host array `out`."""
+        if not isinstance(out, np.ndarray) or not out.flags.c_contiguous:
+            raise ValueError("download_into: out must be a C-contiguous numpy array")
+        self._range(offset, out.nbytes, "download_into")
+        if out.nbytes:
+            check(load().lbf_memcpy_d2h(out.ctypes.data, self.ptr + offset, out.nbytes))
+
     def fill_synthetic(self, seed: int, start: int = 0, nbytes: int | None = None, stream=None, offset: int = 0):
         """Bytes [start, start+nbytes) of synthetic stream `seed` into this
         buffer at byte `offset` (16-byte aligned)."""

@@ -79,10 +79,31 @@ Error::ErrorCode Flood::Initialize(FloodFileSPtr& i_floodfile) {
   return SetupFilesAndChunks();  // Flood.cpp:25-35
 }
 
+// Flood.cpp:243-257: chunk k of the vector (sorted by index in FromXML) starts
+// where chunk k-1 ended.  64-bit offsets; the reference's U32 next_offset
+// wraps past 4 GiB.  False when the indices are not 0..n-1 exactly once (the
+// reference asserts, Flood.cpp:253-254).
+bool Flood::LayoutChunks(const FloodFile::File& i_file, V_U64& o_offsets) {
+  const U64 n = i_file.m_chunks.size();
+  o_offsets.assign(n, 0);
+  std::vector<bool> seen(n, false);
+  U64 next = 0;
+  for (U64 k = 0; k < n; ++k) {
+    const FloodFile::Chunk& c = i_file.m_chunks[k];
+    if (c.m_index >= n || seen[c.m_index]) return false;
+    seen[c.m_index] = true;
+    o_offsets[c.m_index] = next;
+    next += c.m_size;
+  }
+  return true;
+}
+
 // Flood.cpp:220-299.  Per file: lay the chunks out back to back in index
 // order; then hash every chunk of every file that exists on disk in ONE
 // batched verify (lbf_files_ranges).  The reference does fseek + malloc +
-// fread + Base64Encode + strcmp per chunk, file after file.
+// fread + Base64Encode + strcmp per chunk, file after file.  If the batch
+// fails (a HIP error, no memory), each file is verified on its own, and a file
+// whose own call fails too is left out of m_runtimefiles and m_totalbytes.
 Error::ErrorCode Flood::SetupFilesAndChunks() {
   m_totalbytes = 0;
   m_runtimefiles.clear();
@@ -101,55 +122,49 @@ Error::ErrorCode Flood::SetupFilesAndChunks() {
   std::vector<U8> decodable;
   for (const auto& kv : m_floodfile->m_files) {
     const FloodFile::FileSPtr& file = kv.second;
-    m_totalbytes += file->m_size;
     RuntimeFile rtf;
     const U64 n = file->m_chunks.size();
-    rtf.m_chunkoffsets.assign(n, 0);
     rtf.m_chunkmap.assign(n, '0');
     rtf.m_file = file;
-    // offsets follow chunk vector order (sorted by index in FromXML)
-    const U64 first = offs.size();
-    U64 next = 0;
-    bool indices_ok = true;
-    std::vector<bool> seen(n, false);
+    if (!LayoutChunks(*file, rtf.m_chunkoffsets)) {
+      ret = Error::UNKNOWN_ERROR_LBF;
+      continue;
+    }
+    first_of.push_back(offs.size());
     for (U64 k = 0; k < n; ++k) {
       const FloodFile::Chunk& c = file->m_chunks[k];
-      if (c.m_index >= n || seen[c.m_index]) {  // each index 0..n-1 exactly once
-        indices_ok = false;
-        break;
-      }
-      seen[c.m_index] = true;
-      rtf.m_chunkoffsets[c.m_index] = next;
-      offs.push_back(next);
+      offs.push_back(rtf.m_chunkoffsets[c.m_index]);
       sizes.push_back(c.m_size);
       file_of.push_back((U32)paths.size());
       expected.resize(expected.size() + 20, 0);
       decodable.push_back(decode_hash(c.m_hash, &expected[expected.size() - 20]) ? 1 : 0);
-      next += c.m_size;
-    }
-    if (!indices_ok) {  // the reference asserts (Flood.cpp:253-254)
-      offs.resize(first);
-      sizes.resize(first);
-      file_of.resize(first);
-      expected.resize(20 * first);
-      decodable.resize(first);
-      ret = Error::UNKNOWN_ERROR_LBF;
-      continue;
     }
     paths.push_back(PathOf(file->m_name));
-    first_of.push_back(first);
     rtfs.push_back(rtf);
   }
+  first_of.push_back(offs.size());
   V_U8 verdicts(offs.size(), 0);
+  std::vector<U8> file_ok(rtfs.size(), 1);
   std::vector<const char*> cpaths;
   for (const std::string& p : paths) cpaths.push_back(p.c_str());
   if (!offs.empty() && lbf_files_ranges(ctx, cpaths.data(), (U32)cpaths.size(), file_of.data(), offs.data(),
-                                        sizes.data(), offs.size(), expected.data(), verdicts.data()) != LBF_OK)
-    return Error::UNKNOWN_ERROR_LBF;
+                                        sizes.data(), offs.size(), expected.data(), verdicts.data()) != LBF_OK) {
+    ret = Error::UNKNOWN_ERROR_LBF;
+    for (size_t f = 0; f < rtfs.size(); ++f) {  // one file at a time
+      const U64 b = first_of[f], e = first_of[f + 1];
+      if (b == e) continue;
+      const U32 zero = 0;
+      V_U32 fo(e - b, zero);
+      file_ok[f] = lbf_files_ranges(ctx, &cpaths[f], 1, fo.data(), offs.data() + b, sizes.data() + b, e - b,
+                                    expected.data() + 20 * b, verdicts.data() + b) == LBF_OK;
+    }
+  }
   for (size_t f = 0; f < rtfs.size(); ++f) {
+    if (!file_ok[f]) continue;
     RuntimeFile& rtf = rtfs[f];
     const FloodFile::FileSPtr& file = rtf.m_file;
     const U64 first = first_of[f];
+    m_totalbytes += file->m_size;
     for (U64 k = 0; k < file->m_chunks.size(); ++k) {
       const U32 idx = file->m_chunks[k].m_index;
       if (verdicts[first + k] && decodable[first + k]) rtf.m_chunkmap[idx] = '1';

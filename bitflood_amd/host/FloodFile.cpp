@@ -237,7 +237,9 @@ bool chunk_less(const FloodFile::Chunk& a, const FloodFile::Chunk& b) { return a
 
 void FloodFile::SetResolveTrackerHosts(bool i_resolve) { g_resolve_hosts.store(i_resolve); }
 
-Error::ErrorCode FloodFile::ToXML(std::string& o_xml) {
+Error::ErrorCode FloodFile::ToXML(std::string& o_xml) { return ToXML(o_xml, SizeAttr::RefU32); }
+
+Error::ErrorCode FloodFile::ToXML(std::string& o_xml, SizeAttr i_sizes) {
   std::string x;
   x.reserve(128 + 90 * 1024);
   x += "\n<";  // root element at level 0: one newline, no indent
@@ -255,7 +257,9 @@ Error::ErrorCode FloodFile::ToXML(std::string& o_xml) {
       x += "\n    <";
       x += kFile;
       attr(x, "name", f.m_name);
-      attr(x, "size", std::to_string(f.m_size));
+      // RefU32: what the reference's U32 filesize holds after the fread loop
+      // (Encoder.cpp:42,59,76) -- the size modulo 2^32
+      attr(x, "size", std::to_string(i_sizes == SizeAttr::RefU32 ? (U64)(U32)f.m_size : f.m_size));
       if (f.m_chunks.empty()) {
         x += "/>";
         continue;
@@ -323,6 +327,11 @@ Error::ErrorCode FloodFile::FromXML(const std::string& i_xml) {
           f->m_chunks.push_back(c);
         }
         std::stable_sort(f->m_chunks.begin(), f->m_chunks.end(), chunk_less);  // FloodFile.cpp:268
+        // A reference-written (wrapped U32) size of a file >= 4 GiB: the chunk
+        // sizes carry the true total, which the size matches modulo 2^32.
+        U64 sum = 0;
+        for (const Chunk& c : f->m_chunks) sum += c.m_size;
+        if (sum > 0xFFFFFFFFull && f->m_size == (sum & 0xFFFFFFFFull)) f->m_size = sum;
         m_files[f->m_name] = f;
       }
     }
@@ -355,9 +364,9 @@ Error::ErrorCode FloodFile::ComputeHash(std::string& o_hash) {
   return Encoder::Base64Encode(reinterpret_cast<const U8*>(tohash.data()), (U32)tohash.size(), o_hash);
 }
 
-Error::ErrorCode FloodFile::ToXMLFile(const std::string& i_path, bool i_crlf) {
+Error::ErrorCode FloodFile::ToXMLFile(const std::string& i_path, bool i_crlf, SizeAttr i_sizes) {
   std::string xml;
-  ToXML(xml);
+  ToXML(xml, i_sizes);
   if (i_crlf) {
     std::string w;
     w.reserve(xml.size() + xml.size() / 16);

@@ -105,19 +105,22 @@ bool parse_value(const char* s, size_t len, size_t& off, Value& v, U8* dst, size
   bool ok = false;
   if (tag == "<i4>" || tag == "<int>") {
     // intFromXml is strtol on the rest of the buffer; the frame is (ptr, len)
-    // and need not be NUL-terminated, so strtol runs on a bounded copy.  63
-    // chars hold any whitespace + sign + digits strtol would still accept
+    // and need not be NUL-terminated, so strtol runs on a bounded copy.  The
+    // leading whitespace strtol skips (any amount) is skipped in the frame
+    // first; 63 chars then hold any sign + digits strtol would still accept
     // without saturating differently.
+    size_t ws = off;
+    while (ws < len && (s[ws] == ' ' || (s[ws] >= '\t' && s[ws] <= '\r'))) ++ws;
     char tok[64];
-    const size_t n = std::min(sizeof(tok) - 1, len - off);
-    memcpy(tok, s + off, n);
+    const size_t n = std::min(sizeof(tok) - 1, len - ws);
+    memcpy(tok, s + ws, n);
     tok[n] = '\0';
     char* end = nullptr;
     const long x = strtol(tok, &end, 10);
     if (end != tok) {
       v.m_type = Value::INT;
       v.m_int = (int)x;
-      off += (size_t)(end - tok);
+      off = ws + (size_t)(end - tok);
       ok = next_tag_is(tag == "<i4>" ? "</i4>" : "</int>", s, len, off);
     }
   } else if (tag.empty() || tag == "<string>" || tag == "</value>") {

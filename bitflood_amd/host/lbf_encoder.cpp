@@ -8,6 +8,9 @@
 // reference hard-wires to 262144 (:56) becomes a flag (config C1 needs 64 KiB).
 // --crlf writes the CRLF line ends test_encoder's fopen(..., "w") produces on
 // Win32.  --time prints one JSON line: bytes, files, EncodeFile and XML seconds.
+// File sizes: the reference's wrapped U32 by default (--ref-u32-size, the
+// bytes its encoder writes for a file >= 4 GiB); --true-size writes 64-bit
+// sizes instead (FloodFile.H, SizeAttr).
 #include <sys/stat.h>
 
 #include <chrono>
@@ -27,11 +30,14 @@ int main(int argc, char* argv[]) {
   std::vector<std::string> pos;
   U32 chunksize = 262144;
   bool crlf = false, timing = false;
+  FloodFile::SizeAttr sizes = FloodFile::SizeAttr::RefU32;
   for (int i = 1; i < argc; ++i) {
     const std::string a = argv[i];
     if (a == "--chunksize" && i + 1 < argc) chunksize = (U32)strtoul(argv[++i], nullptr, 10);
     else if (a == "--crlf") crlf = true;
     else if (a == "--time") timing = true;
+    else if (a == "--ref-u32-size") sizes = FloodFile::SizeAttr::RefU32;
+    else if (a == "--true-size") sizes = FloodFile::SizeAttr::True64;
     else if (a == "--devices" && i + 1 < argc) Encoder::SetDeviceMask((U32)strtoul(argv[++i], nullptr, 0));
     else pos.push_back(a);
   }
@@ -64,7 +70,7 @@ int main(int argc, char* argv[]) {
     return 2;
   }
   const auto t1 = Clock::now();
-  if (out.ToXMLFile(pos.back(), crlf) != Error::NO_ERROR_LBF) {
+  if (out.ToXMLFile(pos.back(), crlf, sizes) != Error::NO_ERROR_LBF) {
     std::cerr << "cannot write " << pos.back() << std::endl;
     return 3;
   }

@@ -18,6 +18,9 @@
 //    leecher keeps --window requests outstanding;
 //  - batched verify: up to --batch arrivals per GPU launch (Flood::ReceiveChunks)
 //    and up to --batch requests per launch on the seeder (ReadVerifiedChunks).
+//    While a verify runs, the next batch starts when it is full or when its
+//    oldest arrival has waited --deadline-ms (default 10; 0 = only when full),
+//    which bounds the verify latency the batching adds.
 // With --corrupt K the seeder flips one byte of every K-th chunk AFTER its own
 // verify (a wire error); the leecher must reject it and ask again.
 // With --synthetic the seeder holds no file: its chunk bytes come from the
@@ -68,6 +71,7 @@ struct Opts {
   U32 chunksize = 262144;
   U32 window = 512;
   U32 batch = 128;
+  U32 deadline_ms = 10;  // flush a partial batch once its oldest arrival waited this long
   unsigned threads = 8;
   U32 corrupt = 0;
   std::string dir;
@@ -482,6 +486,7 @@ int main(int argc, char** argv) {
     else if (a == "--chunksize") o.chunksize = (U32)strtoul(val(), nullptr, 10);
     else if (a == "--window") o.window = (U32)strtoul(val(), nullptr, 10);
     else if (a == "--batch") o.batch = (U32)strtoul(val(), nullptr, 10);
+    else if (a == "--deadline-ms") o.deadline_ms = (U32)strtoul(val(), nullptr, 10);
     else if (a == "--threads") o.threads = (unsigned)strtoul(val(), nullptr, 10);
     else if (a == "--corrupt") o.corrupt = (U32)strtoul(val(), nullptr, 10);
     else if (a == "--dir") o.dir = val();
@@ -490,7 +495,8 @@ int main(int argc, char** argv) {
     else if (a == "--no-register") o.register_arenas = false;
     else {
       fprintf(stderr,
-              "usage: lbf_loopback [--size BYTES] [--chunksize N] [--window W] [--batch B] [--threads T]\n"
+              "usage: lbf_loopback [--size BYTES] [--chunksize N] [--window W] [--batch B] [--deadline-ms MS]\n"
+              "                    [--threads T]\n"
               "                    [--corrupt K] [--dir DIR] [--keep] [--synthetic] [--no-register]\n");
       return 2;
     }
@@ -685,10 +691,15 @@ int main(int argc, char** argv) {
       if (in_verify == 0) {
         if (!arrivals.cv.wait_for(g, std::chrono::seconds(120), ready)) die("leecher: no chunk arrived for 120 s");
       } else {
-        // a verify is running: start the next batch only once it is full, so
-        // batches grow to what arrives during one verify
-        auto full = [&] { return arrivals.q.size() >= o.batch || arrivals.closed; };
-        if (!arrivals.cv.wait_for(g, std::chrono::milliseconds(1), full)) continue;
+        // a verify is running: start the next batch once it is full (batches
+        // grow to what arrives during one verify), or once its oldest arrival
+        // has waited deadline_ms, which bounds the latency that growth adds
+        const auto deadline = std::chrono::milliseconds(o.deadline_ms);
+        auto due = [&] {
+          return arrivals.q.size() >= o.batch || arrivals.closed ||
+                 (o.deadline_ms > 0 && !arrivals.q.empty() && Clock::now() - arrivals.q.front().t >= deadline);
+        };
+        if (!arrivals.cv.wait_for(g, std::chrono::milliseconds(1), due)) continue;
       }
       while (!arrivals.q.empty() && got.size() < o.batch) {
         got.push_back(std::move(arrivals.q.front()));
@@ -752,14 +763,14 @@ int main(int argc, char** argv) {
   auto pct = [&](double p) { return lat_us.empty() ? 0.0 : lat_us[std::min(lat_us.size() - 1, (size_t)(p * lat_us.size()))]; };
   const double wall = secs(t_start, t_end);
   printf("{\"config\": \"C5 loopback 2-peer\", \"bytes\": %llu, \"chunk_size\": %u, \"chunks\": %zu, "
-         "\"window\": %u, \"batch\": %u, \"threads\": %u, \"seconds\": %.3f, \"payload_gibs\": %.3f, "
+         "\"window\": %u, \"batch\": %u, \"deadline_ms\": %u, \"threads\": %u, \"seconds\": %.3f, \"payload_gibs\": %.3f, "
          "\"wire_gibs\": %.3f, \"encode_flood_s\": %.3f, "
          "\"leecher\": {\"batches\": %zu, \"mean_batch\": %.1f, \"decode_s\": %.3f, \"verify_write_s\": %.3f, "
          "\"rejected\": %zu, \"undecodable\": %zu}, \"seeder\": {\"requests\": %llu, \"sent\": %llu, \"refused\": %llu, \"verify_s\": %.3f, "
          "\"encode_s\": %.3f}, \"verify_latency_us\": {\"p50\": %.0f, \"p90\": %.0f, \"p99\": %.0f, \"max\": %.0f}, "
          "\"resume_verify_complete\": %s, \"files_identical\": %s, \"corrupt_every\": %u, \"corrupted_sent\": %llu, "
          "\"seed_source\": \"%s\", \"arenas_registered\": %s}\n",
-         (unsigned long long)o.size, o.chunksize, total, o.window, o.batch, o.threads, wall,
+         (unsigned long long)o.size, o.chunksize, total, o.window, o.batch, o.deadline_ms, o.threads, wall,
          payload / wall / (1u << 30), wire_bytes / wall / (1u << 30), encode_s, batches,
          batches ? (double)(accepted + rejected) / batches : 0.0, decode_s, verify_s, rejected, undecodable,
          (unsigned long long)sst.requests, (unsigned long long)sst.sent, (unsigned long long)sst.refused, sst.verify_s,

@@ -24,6 +24,7 @@
  */
 #include <pthread.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <string.h>
 #include <stdlib.h>
 
@@ -183,4 +184,31 @@ uint64_t unrolled_clock_probe(uint64_t iters) {
     __asm__ volatile("" : "+r"(x));
   }
   return x;
+}
+
+/* fread-inclusive single-thread encode of one file in Encoder::EncodeFile's
+ * shape (Encoder.cpp:40-79: one chunk_size buffer, fread, hash, repeat), with
+ * this file's hash.  Returns the chunk count, or -1 when the file cannot be
+ * opened. */
+int64_t unrolled_encode_file(const char* path, uint32_t chunk_size, uint8_t* digests, uint64_t max_chunks) {
+  FILE* f = fopen(path, "rb");
+  if (!f || chunk_size == 0) {
+    if (f) fclose(f);
+    return -1;
+  }
+  uint8_t* buf = (uint8_t*)malloc(chunk_size);
+  if (!buf) {
+    fclose(f);
+    return -1;
+  }
+  int64_t idx = 0;
+  for (;;) {
+    size_t got = fread(buf, 1, chunk_size, f);
+    if (got == 0) break;
+    if ((uint64_t)idx < max_chunks) unrolled_sha1(buf, (uint32_t)got, digests + 20 * idx);
+    ++idx;
+  }
+  free(buf);
+  fclose(f);
+  return idx;
 }

@@ -41,6 +41,8 @@ class Oracle:
                                             _c.c_int]
         lib.unrolled_clock_probe.argtypes = [_c.c_uint64]
         lib.unrolled_clock_probe.restype = _c.c_uint64
+        lib.unrolled_encode_file.argtypes = [_c.c_char_p, _c.c_uint32, _c.c_void_p, _c.c_uint64]
+        lib.unrolled_encode_file.restype = _c.c_int64
         self.lib = lib
 
     @staticmethod

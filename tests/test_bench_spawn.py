@@ -1,0 +1,78 @@
+"""bench.py --gpus N with no outside launcher starts its own N rank processes
+(VERDICT r02 "Next round" #1).  On CPU the rank body is tests/spawn_rank_stub.py,
+with the oracle standing in for each rank's GPU: what is under test is the
+spawner -- the world it forms, the environment each rank gets, rank 0's single
+line on stdout, and that a failing rank fails the run instead of leaving the
+others waiting."""
+import json
+import os
+import subprocess
+import sys
+import time
+
+import pytest
+
+import bench
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+STUB = os.path.join(ROOT, "tests", "spawn_rank_stub.py")
+
+
+def _run_spawner(n, env_extra=None, timeout=120):
+    """bench.spawn_ranks in a child Python, so its stdout is capturable."""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LBF_BENCH_BACKEND")}
+    env.update(env_extra or {})
+    code = (f"import sys; sys.path.insert(0, {ROOT!r}); import bench; "
+            f"sys.exit(bench.spawn_ranks({n}, [], script={STUB!r}))")
+    return subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=timeout,
+                          cwd=ROOT)
+
+
+@pytest.mark.parametrize("n", [2, 4])
+def test_spawner_forms_world_and_rank0_prints_one_line(n):
+    p = _run_spawner(n)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [x for x in p.stdout.splitlines() if x.strip()]
+    assert len(lines) == 1, p.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == n
+    assert out["per_rank"] == [1] * n
+    assert out["first_chunk_per_rank"] == [24 * r for r in range(n)]
+    assert out["local_rank"] == list(range(n))
+    assert out["slice_hash_ok"] is True
+    assert out["master"][0] == "127.0.0.1"
+    # no GPU here: fewer devices than ranks -> the spawner picks gloo itself
+    assert out["backend"] == "gloo"
+    assert out["launcher"] == "bench.py"
+
+
+def test_spawner_failing_rank_fails_the_run_and_stops_the_others():
+    t0 = time.time()
+    p = _run_spawner(3, {"STUB_FAIL_RANK": "1"}, timeout=90)
+    assert p.returncode == 3, (p.returncode, p.stderr[-2000:])
+    assert "rank 1 exited with 3" in p.stderr
+    assert p.stdout.strip() == ""
+    assert time.time() - t0 < 60
+
+
+def test_rank_env_matches_torchrun_contract():
+    envs = bench.rank_env({"X": "1"}, 3, 29555, backend="gloo")
+    assert [e["RANK"] for e in envs] == ["0", "1", "2"]
+    assert [e["LOCAL_RANK"] for e in envs] == ["0", "1", "2"]
+    for e in envs:
+        assert e["WORLD_SIZE"] == "3" and e["LOCAL_WORLD_SIZE"] == "3"
+        assert e["MASTER_ADDR"] == "127.0.0.1" and e["MASTER_PORT"] == "29555"
+        assert e["LBF_BENCH_BACKEND"] == "gloo" and e["X"] == "1"
+    assert "LBF_BENCH_BACKEND" not in bench.rank_env({}, 2, 1)[0]
+
+
+def test_world_mismatch_under_outside_launcher_is_refused(monkeypatch):
+    """Under torch.distributed.run with WORLD_SIZE != --gpus the bench refuses to
+    run instead of measuring a different world."""
+    monkeypatch.setenv("WORLD_SIZE", "1")
+    monkeypatch.setenv("RANK", "0")
+
+    class A:
+        gpus = 8
+    with pytest.raises(SystemExit, match="WORLD_SIZE is 1"):
+        bench.dist_setup(A())

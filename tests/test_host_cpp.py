@@ -257,6 +257,61 @@ def test_verify_cli_resume(tmp_path, oracle):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("form", ["default", "--ref-u32-size", "--true-size"])
+def test_encoder_cli_file_past_4gib(tmp_path, form):
+    """A 4 GiB + 12,345 B sparse file at 256 KiB chunks through EncodeFile and the
+    resume verify.  The flood file's size attribute is the reference's wrapped
+    U32 (Encoder.cpp:42,59,76: 12345) unless --true-size; either way lbf_verify
+    reads it back and lays chunk 16,384 out at byte 4 GiB (the reference's U32
+    offset would be 0), so damaging exactly that chunk flips exactly its bit."""
+    cs, size = 262144, (4 << 30) + 12345
+    n = size // cs + 1
+    f = tmp_path / "big.bin"
+    rng = np.random.default_rng(4)
+    marks = {0: rng.integers(0, 256, 1000, dtype=np.uint8), 8192 * cs + 77: rng.integers(0, 256, 5000, dtype=np.uint8),
+             (n - 2) * cs + cs - 300: rng.integers(0, 256, 300, dtype=np.uint8),
+             (n - 1) * cs: rng.integers(0, 256, 12345, dtype=np.uint8)}
+    with open(f, "wb") as fh:
+        fh.truncate(size)
+        for off, b in marks.items():
+            fh.seek(off)
+            fh.write(b.tobytes())
+
+    def chunk_hash(k):
+        b = bytearray(min(cs, size - k * cs))
+        for off, m in marks.items():
+            lo, hi = max(off, k * cs), min(off + m.size, k * cs + len(b))
+            if lo < hi:
+                b[lo - k * cs:hi - k * cs] = m[lo - off:hi - off].tobytes()
+        return b64_27(hashlib.sha1(bytes(b)).digest())
+
+    args = [ENCODER, "big.bin", "http://127.0.0.1:10101/", "big.flood"] + ([] if form == "default" else [form])
+    out = subprocess.run(args, cwd=tmp_path, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    xml = (tmp_path / "big.flood").read_text()
+    want_size = size if form == "--true-size" else size % (1 << 32)
+    assert f'<File name="big.bin" size="{want_size}">' in xml
+    assert xml.count("<Chunk ") == n
+    zero = b64_27(hashlib.sha1(bytes(cs)).digest())
+    for k in (0, 1, 8192, 8193, n - 2, n - 1):
+        want = chunk_hash(k)
+        assert f'<Chunk hash="{want}" index="{k}" size="{min(cs, size - k * cs)}" weight="0"/>' in xml, k
+    assert xml.count(f'hash="{zero}"') == n - 4  # every chunk without a mark is zeros
+
+    def verify():
+        r = subprocess.run([VERIFY, "big.flood", "--no-resolve"], cwd=tmp_path, capture_output=True, text=True,
+                           timeout=300)
+        assert r.returncode == 0, r.stderr
+        return dict(line.split(" ", 1) for line in r.stdout.strip().splitlines())
+
+    assert verify()["big.bin"] == f"{n} {n} " + "1" * n
+    with open(f, "r+b") as fh:  # one byte of the chunk that starts at 4 GiB
+        fh.seek((n - 1) * cs + 6000)
+        fh.write(b"\xff" if marks[(n - 1) * cs][6000] != 0xFF else b"\x00")
+    assert verify()["big.bin"] == f"{n} {n - 1} " + "1" * (n - 1) + "0"
+
+
+@pytest.mark.gpu
 def test_cpp_api_gpu_suite(tmp_path):
     out = subprocess.run([os.path.join(LIB, "lbf_gpu_tests"), str(tmp_path)], capture_output=True, text=True)
     assert out.returncode == 0, out.stderr + out.stdout
