@@ -302,7 +302,7 @@ def cpu_baseline(args, stream_start, n_chunks_sample, gpu_digests_sample):
     def rate(fn, nthreads, n=n_chunks_sample, min_s=3.0, max_reps=20):
         reps, t = 0, 0.0
         d = None
-        while t < min_s and reps < max_reps:
+        while reps == 0 or (t < min_s and reps < max_reps):
             t0 = time.perf_counter()
             d = fn(data, offs[:n], sizes[:n], nthreads=nthreads)
             t += time.perf_counter() - t0

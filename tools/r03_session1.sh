@@ -6,9 +6,9 @@ set -o pipefail
 O=gpurun_out/r03/s1
 mkdir -p $O
 T="timeout -k 10"
-$T 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
+{ [ -n "$SKIP_PYTEST" ] || $T 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
     tests/test_gpu_files.py "tests/test_host_cpp.py::test_encoder_cli_file_past_4gib" \
-    tests/test_gpu_parity.py tests/test_gpu_registered.py -m gpu > $O/pytest_new.log 2>&1 &&
+    tests/test_gpu_parity.py tests/test_gpu_registered.py -m gpu > $O/pytest_new.log 2>&1; } &&
 $T 300 python -u bench.py > $O/bench_c2_n1.json 2> $O/bench_c2_n1.err &&
 LBF_BENCH_BACKEND=gloo $T 300 python -u bench.py --gpus 2 > $O/bench_c2_n2_spawned.json 2> $O/bench_c2_n2_spawned.err &&
 LBF_WORKERS_PER_DEVICE=2 $T 300 python -u bench.py --gpus 2 > $O/bench_c2_n2_spawned_w2.json 2> $O/bench_c2_n2_spawned_w2.err &&
