@@ -8,4 +8,9 @@ mkdir -p $O
 T="timeout -k 10"
 LBF_BENCH_BACKEND=gloo $T 600 python -u bench.py --gpus 8 --config c4 > $O/bench_c4_n8_spawned.json 2> $O/bench_c4_n8_spawned.err &&
 $T 300 python -u bench.py > $O/bench_c2_n1.json 2> $O/bench_c2_n1.err &&
-bash tools/profile_round.sh c2_r03 > $O/profile_c2.txt 2>&1
+bash tools/profile_round.sh c2_r03 > $O/profile_c2.txt 2>&1 &&
+# host ASan/UBSan over the C ABI with the many-file windows forced small
+# (LBF_FILES_WINDOW=2: every multi-file verify job runs in windows)
+bash tools/asan_build.sh > $O/asan_build.txt 2>&1 &&
+mkdir -p /tmp/asan_scratch &&
+LBF_FILES_WINDOW=2 ASAN_OPTIONS=detect_leaks=0 $T 200 tools/build/asan/asan_capi /tmp/asan_scratch 90 93 > $O/asan_windows_seed93.txt 2>&1
