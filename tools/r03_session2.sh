@@ -6,6 +6,7 @@ set -o pipefail
 O=gpurun_out/r03/s2
 mkdir -p $O
 T="timeout -k 10"
+$T 300 python -u -m pytest -x -v --timeout 240 --timeout-method thread tests/test_gpu_bench_ranks.py -m gpu > $O/pytest_bench_ranks.txt 2>&1 &&
 LBF_BENCH_BACKEND=gloo $T 600 python -u bench.py --gpus 8 --config c4 > $O/bench_c4_n8_spawned.json 2> $O/bench_c4_n8_spawned.err &&
 $T 300 python -u bench.py > $O/bench_c2_n1.json 2> $O/bench_c2_n1.err &&
 bash tools/profile_round.sh c2_r03 > $O/profile_c2.txt 2>&1 &&
