@@ -675,8 +675,8 @@ def main():
 
     # N>1: the copy-inclusive rate with every rank pulling from host memory at once
     e2e_multi = None
-    slice_bytes = min(file_bytes, E2E_SLICE_BYTES)
-    n_slice = slice_bytes // cs
+    n_slice = min(file_bytes, E2E_SLICE_BYTES) // cs  # whole chunks only
+    slice_bytes = n_slice * cs
     if world > 1:
         # the host slice, then free the shard's HBM before the host-memory legs:
         # with ranks sharing a GPU (rehearsals: 8 x 32 GiB of C4 on one card)
@@ -684,7 +684,7 @@ def main():
         host = buf.download(slice_bytes) if not args.no_e2e else None
         buf.free()
         buf = None
-    if world > 1 and not args.no_e2e:
+    if world > 1 and not args.no_e2e and n_slice:
         r = e2e_leg(host, cs, dev, world)
         del host
         ok = int(np.array_equal(r["digests"], digests[:n_slice]) and r["registered_equal"])
@@ -813,7 +813,7 @@ def main():
         import torch.distributed as dist
         barrier(world)  # every rank's e2e leg has ended before rank 0 goes on alone
         dist.destroy_process_group()
-    if rank == 0 and world > 1 and not args.no_e2e and not args.no_inproc:
+    if rank == 0 and world > 1 and not args.no_e2e and not args.no_inproc and n_slice:
         gen = None
         try:
             gen = DeviceBuffer(slice_bytes)
