@@ -41,19 +41,31 @@ def main():
     ap.add_argument("dst")
     ap.add_argument("--file-bytes", type=int, default=4 << 30)
     ap.add_argument("--chunk-size", type=int, default=262144)
-    ap.add_argument("--kernel", default="sha1_")
+    ap.add_argument("--kernel", default=None,
+                    help="kernel name substring; default: the kernel the traced bench line names (config.kernel)")
     ap.add_argument("--record", action="store_true")
     a = ap.parse_args()
+    if a.kernel is None:
+        a.kernel = "sha1_"
+        try:  # the bench's own line in the traced run names its device-resident kernel
+            for line in open(os.path.join(a.src, "trace.log")):
+                if line.startswith("{"):
+                    a.kernel = json.loads(line)["config"]["kernel"]
+        except (OSError, ValueError, KeyError):
+            pass
     os.makedirs(a.dst, exist_ok=True)
     out = {"file_bytes": a.file_bytes}
 
     stats = os.path.join(a.src, "trace", "trace_kernel_stats.csv")
     if os.path.exists(stats):
         shutil.copy(stats, os.path.join(a.dst, "kernel_stats.csv"))
-        for r in csv.DictReader(open(stats)):
-            # rows are sorted by total time: keep the first match (the bench's
-            # device-resident kernel, not the host path's e2e launches)
-            if a.kernel in r["Name"] and "kernel" not in out:
+        rows = [r for r in csv.DictReader(open(stats)) if a.kernel in r["Name"]]
+        # the bench's device-resident launches are the uniform-mode kernels
+        # (`<true, ...>`); the host legs' batches (`<false, ...>`) can total more
+        # time since round 3's e2e passes, so prefer uniform mode, then total time
+        rows.sort(key=lambda r: "<true" not in r["Name"])
+        for r in rows:
+            if "kernel" not in out:
                 out["kernel"] = r["Name"]
                 out["trace_avg_ns"] = float(r["AverageNs"])
                 out["trace_calls"] = int(r["Calls"])
@@ -63,7 +75,7 @@ def main():
         if not os.path.exists(p):
             return {}, {}
         agg, durs = per_kernel(p)
-        for k in agg:
+        for k in sorted(agg, key=lambda k: "<true" not in k):
             if a.kernel in k:
                 return agg[k], durs[k]
         return {}, {}
