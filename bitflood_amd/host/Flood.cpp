@@ -356,11 +356,21 @@ Error::ErrorCode Flood::VerifyChunks(const U8* i_arena, U64 i_arena_len, const s
 
 Error::ErrorCode Flood::ReceiveChunks(const U8* i_arena, U64 i_arena_len, const std::vector<ChunkArrival>& i_chunks,
                                       std::string& o_accepted) {
-  const size_t n = i_chunks.size();
-  o_accepted.assign(n, '0');
+  o_accepted.assign(i_chunks.size(), '0');
   std::string valid;
   const Error::ErrorCode rc = VerifyChunks(i_arena, i_arena_len, i_chunks, valid);
   if (rc != Error::NO_ERROR_LBF) return rc;
+  return WriteChunks(i_arena, i_chunks, valid, o_accepted);
+}
+
+// ChunkMethods.cpp:169-185: write each chunk whose verdict is '1' at its
+// offset, then mark it '1' and drop it from the download set.
+Error::ErrorCode Flood::WriteChunks(const U8* i_arena, const std::vector<ChunkArrival>& i_chunks,
+                                    const std::string& i_valid, std::string& o_accepted) {
+  const size_t n = i_chunks.size();
+  o_accepted.assign(n, '0');
+  if (i_valid.size() != n) return Error::UNKNOWN_ERROR_LBF;
+  const std::string& valid = i_valid;
   std::vector<size_t> which;
   for (size_t k = 0; k < n; ++k)
     if (valid[k] == '1') which.push_back(k);

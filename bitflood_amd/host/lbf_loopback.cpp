@@ -31,7 +31,8 @@
 // 16 GiB C5 transfer needs 16 GiB of scratch space, not 32; the written file is
 // compared with the generator instead of a source file.
 //
-// Prints one JSON line: payload rate, verify latency, batch sizes, and the end
+// Prints one JSON line: payload rate, verify latency (frame arrival -> GPU
+// verdict) and accept latency (arrival -> chunk written), batch sizes, and the end
 // state (resume verify of the written file, byte comparison with the source).
 #include <arpa/inet.h>
 #include <fcntl.h>
@@ -557,7 +558,7 @@ int main(int argc, char** argv) {
   std::deque<Flood::P_ChunkKey> todo(fl.m_chunkstodownload.begin(), fl.m_chunkstodownload.end());
   const std::vector<Flood::P_ChunkKey> all_keys(todo.begin(), todo.end());
   const size_t total = todo.size();
-  constexpr int kArenas = 3;
+  constexpr int kArenas = 4;  // one filling, one in GPU verify, one queued for it, one being written
   const U64 slot = ((U64)o.chunksize + 15) & ~15ull;
   // The arenas live for the whole transfer: pinned once, each batch's verify
   // copies them straight to HBM instead of through the context's staging
@@ -585,19 +586,24 @@ int main(int argc, char** argv) {
   const int fd = connect_loopback(port);
 
   // Leecher pipeline: reader thread (frames), this thread (decode into one of
-  // kArenas arenas, bookkeeping, requests), verifier thread (ReceiveChunks:
-  // GPU verify + write), so a batch's verify overlaps the next batch's decode.
+  // kArenas arenas, bookkeeping, requests), verifier thread (VerifyChunks: the
+  // GPU verify, the verdict), writer thread (WriteChunks: the accepted chunks
+  // to disk, chunkmap '1').  ReceiveChunks split in two, so a batch's verify
+  // overlaps the next batch's decode and the previous batch's writes, and a
+  // slow disk does not hold up verdicts.
   struct Batch {
     std::vector<Arrival> got;
     std::vector<Flood::ChunkArrival> arr;
     std::vector<size_t> pos;
     int arena = 0;
     std::string acc;
-    Clock::time_point done;
-    double verify_s = 0;
+    std::string valid;
+    Clock::time_point verdict, done;
+    double verify_s = 0, write_s = 0;
   };
   Chan<Arrival> arrivals;
-  Chan<Batch> to_verify, verified;
+  Chan<Batch> to_verify, to_write, verified;
+  std::atomic<size_t> in_gpu{0};  // batches handed to the verifier and not yet verified
   std::thread reader([&] {
     FrameReader rd(fd);
     std::string f;
@@ -609,19 +615,34 @@ int main(int argc, char** argv) {
     while (to_verify.take(bs, 1)) {
       Batch& b = bs[0];
       auto v0 = Clock::now();
-      if (fl.ReceiveChunks(arenas[b.arena].data(), arenas[b.arena].size(), b.arr, b.acc) != Error::NO_ERROR_LBF)
-        die("leecher: ReceiveChunks failed: " + std::string(Encoder::LastError()));
+      if (fl.VerifyChunks(arenas[b.arena].data(), arenas[b.arena].size(), b.arr, b.valid) != Error::NO_ERROR_LBF)
+        die("leecher: VerifyChunks failed: " + std::string(Encoder::LastError()));
+      b.verdict = Clock::now();
+      b.verify_s = secs(v0, b.verdict);
+      --in_gpu;
+      to_write.put(std::move(b));
+    }
+    to_write.close();
+  });
+  std::thread writer([&] {
+    std::vector<Batch> bs;
+    while (to_write.take(bs, 1)) {
+      Batch& b = bs[0];
+      auto w0 = Clock::now();
+      if (fl.WriteChunks(arenas[b.arena].data(), b.arr, b.valid, b.acc) != Error::NO_ERROR_LBF)
+        die("leecher: WriteChunks failed");
       b.done = Clock::now();
-      b.verify_s = secs(v0, b.done);
+      b.write_s = secs(w0, b.done);
       verified.put(std::move(b));
     }
   });
 
-  std::vector<double> lat_us;
+  std::vector<double> lat_us, acc_us;  // arrival -> verdict, arrival -> written
   lat_us.reserve(total);
+  acc_us.reserve(total);
   size_t inflight = 0, accepted = 0, rejected = 0, batches = 0, wire_bytes = 0, undecodable = 0;
   U64 payload = 0;
-  double decode_s = 0, verify_s = 0;
+  double decode_s = 0, verify_s = 0, write_s = 0;
   Flood::S_ChunkKey done;
   std::vector<int> free_arenas;
   for (int a = 0; a < kArenas; ++a) free_arenas.push_back(a);
@@ -643,9 +664,11 @@ int main(int argc, char** argv) {
   auto settle = [&](Batch& b) {
     ++batches;
     verify_s += b.verify_s;
+    write_s += b.write_s;
     inflight -= b.got.size();
     for (size_t j = 0; j < b.arr.size(); ++j) {
-      lat_us.push_back(secs(b.got[b.pos[j]].t, b.done) * 1e6);
+      lat_us.push_back(secs(b.got[b.pos[j]].t, b.verdict) * 1e6);
+      acc_us.push_back(secs(b.got[b.pos[j]].t, b.done) * 1e6);
       const Flood::P_ChunkKey key(b.arr[j].m_filename, b.arr[j].m_index);
       if (b.acc[j] == '1') {
         if (done.insert(key).second) {
@@ -691,13 +714,19 @@ int main(int argc, char** argv) {
       if (in_verify == 0) {
         if (!arrivals.cv.wait_for(g, std::chrono::seconds(120), ready)) die("leecher: no chunk arrived for 120 s");
       } else {
-        // a verify is running: start the next batch once it is full (batches
-        // grow to what arrives during one verify), or once its oldest arrival
-        // has waited deadline_ms, which bounds the latency that growth adds
+        // Batches are in flight.  With the GPU idle (they are only being
+        // written), start at once.  With one verify running, start the next
+        // batch once it is full (batches grow to what arrives during one
+        // verify) or once its oldest arrival has waited deadline_ms, which
+        // bounds the latency that growth adds.  With a batch already queued
+        // behind that verify, only a full batch goes: a smaller one would wait
+        // for the GPU anyway, and would cost one more chain of verify time.
+        const size_t gq = in_gpu.load();
         const auto deadline = std::chrono::milliseconds(o.deadline_ms);
         auto due = [&] {
-          return arrivals.q.size() >= o.batch || arrivals.closed ||
-                 (o.deadline_ms > 0 && !arrivals.q.empty() && Clock::now() - arrivals.q.front().t >= deadline);
+          if (arrivals.q.size() >= o.batch || arrivals.closed) return true;
+          if (arrivals.q.empty()) return false;
+          return gq == 0 || (gq == 1 && o.deadline_ms > 0 && Clock::now() - arrivals.q.front().t >= deadline);
         };
         if (!arrivals.cv.wait_for(g, std::chrono::milliseconds(1), due)) continue;
       }
@@ -739,11 +768,13 @@ int main(int argc, char** argv) {
     b.got = std::move(got);
     got = std::vector<Arrival>();
     ++in_verify;
+    ++in_gpu;
     to_verify.put(std::move(b));
   }
   const auto t_end = Clock::now();
   to_verify.close();
   verifier.join();
+  writer.join();
   if (o.register_arenas)
     for (const Arena& a : arenas) (void)lbf_host_unregister(leech_ctx, a.data());
   free(arena_mem);
@@ -760,21 +791,28 @@ int main(int argc, char** argv) {
   const bool same = o.synthetic ? file_matches_synthetic(leechdir + "/" + name, o.size, o.threads)
                                 : files_equal(seeddir + "/" + name, leechdir + "/" + name);
   std::sort(lat_us.begin(), lat_us.end());
-  auto pct = [&](double p) { return lat_us.empty() ? 0.0 : lat_us[std::min(lat_us.size() - 1, (size_t)(p * lat_us.size()))]; };
+  std::sort(acc_us.begin(), acc_us.end());
+  auto pct_of = [](const std::vector<double>& v, double p) {
+    return v.empty() ? 0.0 : v[std::min(v.size() - 1, (size_t)(p * v.size()))];
+  };
+  auto pct = [&](double p) { return pct_of(lat_us, p); };
   const double wall = secs(t_start, t_end);
   printf("{\"config\": \"C5 loopback 2-peer\", \"bytes\": %llu, \"chunk_size\": %u, \"chunks\": %zu, "
          "\"window\": %u, \"batch\": %u, \"deadline_ms\": %u, \"threads\": %u, \"seconds\": %.3f, \"payload_gibs\": %.3f, "
          "\"wire_gibs\": %.3f, \"encode_flood_s\": %.3f, "
-         "\"leecher\": {\"batches\": %zu, \"mean_batch\": %.1f, \"decode_s\": %.3f, \"verify_write_s\": %.3f, "
+         "\"leecher\": {\"batches\": %zu, \"mean_batch\": %.1f, \"decode_s\": %.3f, \"verify_s\": %.3f, "
+         "\"write_s\": %.3f, "
          "\"rejected\": %zu, \"undecodable\": %zu}, \"seeder\": {\"requests\": %llu, \"sent\": %llu, \"refused\": %llu, \"verify_s\": %.3f, "
          "\"encode_s\": %.3f}, \"verify_latency_us\": {\"p50\": %.0f, \"p90\": %.0f, \"p99\": %.0f, \"max\": %.0f}, "
+         "\"accept_latency_us\": {\"p50\": %.0f, \"p90\": %.0f, \"p99\": %.0f, \"max\": %.0f}, "
          "\"resume_verify_complete\": %s, \"files_identical\": %s, \"corrupt_every\": %u, \"corrupted_sent\": %llu, "
          "\"seed_source\": \"%s\", \"arenas_registered\": %s}\n",
          (unsigned long long)o.size, o.chunksize, total, o.window, o.batch, o.deadline_ms, o.threads, wall,
          payload / wall / (1u << 30), wire_bytes / wall / (1u << 30), encode_s, batches,
-         batches ? (double)(accepted + rejected) / batches : 0.0, decode_s, verify_s, rejected, undecodable,
+         batches ? (double)(accepted + rejected) / batches : 0.0, decode_s, verify_s, write_s, rejected, undecodable,
          (unsigned long long)sst.requests, (unsigned long long)sst.sent, (unsigned long long)sst.refused, sst.verify_s,
-         sst.encode_s, pct(0.5), pct(0.9), pct(0.99), lat_us.empty() ? 0.0 : lat_us.back(), resumed ? "true" : "false",
+         sst.encode_s, pct(0.5), pct(0.9), pct(0.99), lat_us.empty() ? 0.0 : lat_us.back(), pct_of(acc_us, 0.5),
+         pct_of(acc_us, 0.9), pct_of(acc_us, 0.99), acc_us.empty() ? 0.0 : acc_us.back(), resumed ? "true" : "false",
          same ? "true" : "false", o.corrupt, (unsigned long long)sst.corrupted,
          o.synthetic ? "synthetic stream (generated on request, no seeder file)" : "file",
          o.register_arenas ? "true" : "false");
