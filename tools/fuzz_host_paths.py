@@ -5,7 +5,9 @@ tools/fuzz_gpu.py varies the kernels; this varies what feeds them: staging slot
 sizes (1, 3, 16, 512 MiB, so batches split into many groups and chunks larger
 than a slot take the oversize path), chunk sizes up to 40 MiB, memory vs file
 sources (pread), truncated and missing files in verify mode, device-pointer
-batches, and memory registered with the context (the direct route).  The copy-thread count is process-wide (LBF_COPY_THREADS), so run the
+batches, memory registered with the context (the direct route), and (mode 7)
+multi-file batches (lbf_files_ranges) over 2-40 files, some missing in verify
+mode, with a random LBF_FILES_WINDOW so floods run in windows of files.  The copy-thread count is process-wide (LBF_COPY_THREADS), so run the
 tool once per setting.  Everything is checked against the oracle restatement.
 
 Usage: LBF_COPY_THREADS=3 python tools/fuzz_host_paths.py [--seconds 60] [--seed 1]
@@ -72,14 +74,62 @@ def registered_case(rng, slot, mode, orc, h, pool):
         h.unregister_host(src)
 
 
+def files_case(rng, slot, orc, h, pool, tmpdir):
+    """Mode 7: one lbf_files_ranges call over k files cut from the pool, chunks
+    listed in a shuffled order, with LBF_FILES_WINDOW drawn per case (read by
+    the library on every call), hash or verify (a few files missing)."""
+    k = int(rng.integers(2, 41))
+    lo = int(rng.integers(0, pool.size // 2))
+    cuts = np.sort(rng.integers(lo, min(pool.size, lo + (64 << 20)) + 1, k + 1))
+    paths, fo, offs, sizes, srcs = [], [], [], [], []
+    for f in range(k):
+        data = pool[cuts[f]:cuts[f + 1]]
+        p = os.path.join(tmpdir, f"m{f:02d}.bin")
+        data.tofile(p)
+        paths.append(p)
+        cs = int(rng.choice([4096, 65536, 262144, 1 << 20]))
+        for o in range(0, data.size, cs):
+            fo.append(f)
+            offs.append(o)
+            sizes.append(min(cs, data.size - o))
+            srcs.append(int(cuts[f]) + o)
+    n = len(fo)
+    if n == 0:
+        return slot, 7, 0, True
+    order = rng.permutation(n)
+    fo, offs, sizes, srcs = [np.array(x)[order] for x in (fo, offs, sizes, srcs)]
+    want = orc.sha1_batch(pool, srcs.astype(np.uint64), sizes.astype(np.uint32), nthreads=THREADS)
+    os.environ["LBF_FILES_WINDOW"] = str(int(rng.integers(1, k + 3)))
+    try:
+        if rng.random() < 0.5:
+            ok = bool(np.array_equal(h.hash_files(paths, fo, offs, sizes), want))
+        else:
+            gone = rng.random(k) < 0.2
+            for f in np.nonzero(gone)[0]:
+                os.remove(paths[f])
+            exp = want.copy()
+            bad = rng.random(n) < 0.1
+            exp[bad, 0] ^= np.uint8(1)
+            expect = ~bad & ~gone[fo]
+            ok = bool(np.array_equal(h.verify_files(paths, fo, offs, sizes, exp), expect))
+    finally:
+        os.environ.pop("LBF_FILES_WINDOW", None)
+        for p in paths:
+            if os.path.exists(p):
+                os.remove(p)
+    return slot, 7, n, ok
+
+
 def one_case(seed, orc, hashers, pool, path, tmpdir):
     rng = np.random.default_rng(seed)
     slot = int(rng.choice(SLOTS_MB))
     h = hashers[slot]
     # 0 mem hash, 1 mem verify, 2 file hash, 3 file verify, 4 device ptrs,
     # 5/6 mem hash/verify from a registered source (lbf_host_register) that
-    # starts at a random byte of the pool
-    mode = int(rng.integers(0, 7))
+    # starts at a random byte of the pool, 7 multi-file batches in windows
+    mode = int(rng.integers(0, 8))
+    if mode == 7:
+        return files_case(rng, slot, orc, h, pool, tmpdir)
     if mode >= 5:
         return registered_case(rng, slot, mode, orc, h, pool)
     offs, sizes = draw_table(rng, pool.size)
