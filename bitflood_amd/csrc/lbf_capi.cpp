@@ -27,8 +27,10 @@
 #include <cerrno>
 #include <cstdio>
 #include <cstdlib>
+#include <functional>
 #include <iterator>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <new>
 #include <stdexcept>
@@ -366,6 +368,89 @@ struct DevSlot {
   uint64_t g_begin = 0, g_end = 0;
 };
 
+// Helper threads of one worker's staging copies, started once and kept: a
+// staging piece (LBF_PIN_MB, 128 MiB) moves in ≈2.5 ms at PCIe rate, and
+// starting, binding and joining seven threads for every piece cost a
+// measurable share of that.  run() hands the helpers a piece count and a
+// function, joins in itself, and returns once every helper is done with it.
+class CopyPool {
+ public:
+  CopyPool(unsigned helpers, const std::vector<int>& cpus) {
+    for (unsigned t = 0; t < helpers; ++t) {
+      try {
+        th_.emplace_back([this, cpus] {
+          bind_thread(cpus);
+          loop();
+        });
+      } catch (const std::system_error&) {
+        break;  // fewer helpers: the caller and the others take their pieces
+      }
+    }
+  }
+  ~CopyPool() {
+    {
+      std::lock_guard<std::mutex> lock(mu_);
+      stop_ = true;
+    }
+    cv_work_.notify_all();
+    for (std::thread& t : th_) t.join();
+  }
+  CopyPool(const CopyPool&) = delete;
+  CopyPool& operator=(const CopyPool&) = delete;
+
+  size_t helpers() const { return th_.size(); }
+
+  // fn(q) for q in [0, n), spread over the caller and the helpers
+  void run(size_t n, const std::function<void(size_t)>& fn) {
+    {
+      std::lock_guard<std::mutex> lock(mu_);
+      fn_ = &fn;
+      n_ = n;
+      next_.store(0);
+      busy_ = th_.size();
+      ++gen_;
+    }
+    cv_work_.notify_all();
+    pull(fn, n);
+    std::unique_lock<std::mutex> lock(mu_);
+    cv_done_.wait(lock, [this] { return busy_ == 0; });
+    fn_ = nullptr;
+  }
+
+ private:
+  void pull(const std::function<void(size_t)>& fn, size_t n) {
+    for (size_t q; (q = next_++) < n;) fn(q);
+  }
+  void loop() {
+    uint64_t seen = 0;
+    for (;;) {
+      const std::function<void(size_t)>* fn;
+      size_t n;
+      {
+        std::unique_lock<std::mutex> lock(mu_);
+        cv_work_.wait(lock, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+        fn = fn_;
+        n = n_;
+      }
+      pull(*fn, n);
+      std::lock_guard<std::mutex> lock(mu_);
+      if (--busy_ == 0) cv_done_.notify_one();
+    }
+  }
+
+  std::vector<std::thread> th_;
+  std::mutex mu_;
+  std::condition_variable cv_work_, cv_done_;
+  const std::function<void(size_t)>* fn_ = nullptr;
+  size_t n_ = 0;
+  std::atomic<size_t> next_{0};
+  size_t busy_ = 0;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
+
 struct Worker {
   int device = 0;
   int index = 0;            // position in the context
@@ -384,6 +469,7 @@ struct Worker {
   uint64_t bytes_direct = 0;  // chunk bytes sent straight from registered caller memory
   long fault_group = -1;    // LBF_TEST_FAULT_GROUP (tests only, one shot)
   bool fault_throws = false;  // LBF_TEST_FAULT_KIND=throw: the fault is a host exception, not a HIP error
+  std::unique_ptr<CopyPool> pool;  // staging copy helpers, started by the first job that needs them
 };
 
 }  // namespace
@@ -570,6 +656,7 @@ int worker_init(Worker& w, int device, int index) {
 }
 
 void worker_free(Worker& w) {
+  w.pool.reset();  // idle between jobs: the helpers only need waking and joining
   if (hipSetDevice(w.device) != hipSuccess) return;
   // teardown: errors here have nowhere to go, the context is being destroyed
   for (DevSlot& d : w.dev) dev_slot_free(d);
@@ -628,13 +715,14 @@ struct Run {
 // Copy every run of a group into the slot's data area.  A single host thread
 // copies ~17 GiB/s into pinned memory, a third of what PCIe Gen5 moves, so
 // runs are cut into pieces of at most `step` bytes (≥ 8 MiB of work per
-// thread; `step` rounded up to a page) that up to `threads` threads, bound to
-// the staging's NUMA node, pull from a shared index: one long contiguous run
+// thread; `step` rounded up to a page) that the caller and the worker's
+// CopyPool helpers, bound to the staging's NUMA node, pull from a shared
+// index: one long contiguous run
 // and many small scattered ones copy in parallel alike.  (The ceil(total /
 // parts) step must cover everything: rounding floor(len / parts) once left the
 // last bytes of a range uncopied, tools/fuzz_gpu.py seed 23006099, pinned by
 // test_staging_split_covers_tail.)
-void read_runs(const Source& src, std::vector<Run>& runs, uint8_t* data, const std::vector<int>& cpus) {
+void read_runs(const Source& src, std::vector<Run>& runs, uint8_t* data, Worker& w) {
   constexpr uint64_t kMinPart = 8ull << 20;
   uint64_t total = 0;
   for (const Run& r : runs) total += r.len;
@@ -651,28 +739,37 @@ void read_runs(const Source& src, std::vector<Run>& runs, uint8_t* data, const s
   std::vector<Piece> pieces;
   for (size_t k = 0; k < runs.size(); ++k)
     for (uint64_t a = 0; a < runs[k].len; a += step) pieces.push_back({k, a, std::min(step, runs[k].len - a), 0});
-  std::atomic<size_t> next{0};
-  auto pull = [&] {
-    for (size_t q; (q = next++) < pieces.size();) {
-      Piece& pc = pieces[q];
-      pc.got = src.read_serial(data + runs[pc.run].dst + pc.at, runs[pc.run].file, runs[pc.run].src + pc.at, pc.len);
-    }
+  const std::function<void(size_t)> copy = [&](size_t q) {
+    Piece& pc = pieces[q];
+    pc.got = src.read_serial(data + runs[pc.run].dst + pc.at, runs[pc.run].file, runs[pc.run].src + pc.at, pc.len);
   };
-  // parts - 1 helpers plus the calling thread (already bound by its worker);
-  // a helper that cannot be started leaves its pieces to the others
-  std::vector<std::thread> th;
-  for (uint64_t t = 1; t < parts; ++t) {
-    try {
-      th.emplace_back([&] {
-        bind_thread(cpus);
-        pull();
-      });
-    } catch (const std::system_error&) {
-      break;
+  static const bool use_pool = env_long("LBF_COPY_POOL", 1) != 0;  // 0: threads per call (A/B knob)
+  if (use_pool) {
+    // the worker's helpers (copy_threads() - 1 of them, bound to its node) plus
+    // the calling thread, already bound by its worker
+    if (!w.pool) w.pool.reset(new CopyPool(copy_threads() - 1, w.cpus));
+    w.pool->run(pieces.size(), copy);
+  } else {
+    std::atomic<size_t> next{0};
+    auto pull = [&] {
+      for (size_t q; (q = next++) < pieces.size();) copy(q);
+    };
+    // parts - 1 helpers plus the calling thread; a helper that cannot be
+    // started leaves its pieces to the others
+    std::vector<std::thread> th;
+    for (uint64_t t = 1; t < parts; ++t) {
+      try {
+        th.emplace_back([&] {
+          bind_thread(w.cpus);
+          pull();
+        });
+      } catch (const std::system_error&) {
+        break;
+      }
     }
+    pull();
+    for (auto& t : th) t.join();
   }
-  pull();
-  for (auto& t : th) t.join();
   // a run's readable prefix: its pieces in order up to the first short one
   std::vector<bool> short_seen(runs.size(), false);
   for (Run& r : runs) r.avail = 0;
@@ -733,7 +830,7 @@ int run_oversize(Worker& w, const Job& job, uint64_t i) {
   const uint32_t sz = job.sizes[i];
   std::vector<uint8_t> host(sz ? sz : 1);
   std::vector<Run> one{Run{job.offsets[i], sz, 0, 0, job.file(i)}};
-  read_runs(job.src, one, host.data(), w.cpus);
+  read_runs(job.src, one, host.data(), w);
   const bool ok = one[0].avail == sz && job.src.exists(job.file(i));
   if (!ok) {
     if (job.expected) {
@@ -986,7 +1083,7 @@ int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
           parts.push_back(Run{runs[r].src + (a0 - runs[r].dst), a1 - a0, a0 - pstart, 0, runs[r].file});
           part_of.push_back(r);
         }
-        read_runs(job.src, parts, piece, w.cpus);
+        read_runs(job.src, parts, piece, w);
         for (size_t q = 0; q < parts.size(); ++q) {
           Run& r = runs[part_of[q]];
           r.avail += parts[q].avail;

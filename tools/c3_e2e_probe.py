@@ -36,6 +36,7 @@ ap.add_argument("--files", type=int, default=64, help="first N files of c3.json"
 ap.add_argument("--cli-runs", type=int, default=2)
 ap.add_argument("--threads", type=int, default=8)
 ap.add_argument("--skip", default="", help="comma list of phases to skip: cli,inproc,pread")
+ap.add_argument("--order", default="cli,inproc,pread", help="the phases in the order they run")
 a = ap.parse_args()
 skip = set(filter(None, a.skip.split(",")))
 
@@ -78,7 +79,7 @@ try:
             raise SystemExit(f"{what}: digests differ from c3.json")
         return ok
 
-    if "cli" not in skip:
+    def phase_cli():
         lib = os.path.join(ROOT, "bitflood_amd", "lib")
         for r in range(a.cli_runs):
             out = subprocess.run([os.path.join(lib, "lbf_encoder"), *[os.path.basename(n) for n in names],
@@ -92,7 +93,8 @@ try:
     o, s = chunk_table(fs, cs)
     file_of = np.repeat(np.arange(len(names), dtype=np.uint32), o.size)
     offs, sizes = np.tile(o, len(names)), np.tile(s, len(names))
-    if "inproc" not in skip:
+
+    def phase_inproc():
         t = time.perf_counter()
         with ChunkHasher(device_mask=1) as h:
             t_ctx = time.perf_counter() - t
@@ -112,7 +114,7 @@ try:
               "first_gibs": round(total / GIB / t_first, 2), "best_s": round(best, 3),
               "best_gibs": round(total / GIB / best, 2), "staging": st, "placement": place})
 
-    if "pread" not in skip:
+    def phase_pread():
         dst = np.empty(fs * min(8, len(names)), dtype=np.uint8)  # 8 GiB window, reused
 
         def reader(k0, step):
@@ -139,5 +141,10 @@ try:
                 x.join()
             dt = time.perf_counter() - t
             emit({"phase": "pread", "rep": rep, "threads": a.threads, "gibs": round(total / GIB / dt, 2)})
+
+    phases = {"cli": phase_cli, "inproc": phase_inproc, "pread": phase_pread}
+    for name in a.order.split(","):
+        if name not in skip:
+            phases[name]()
 finally:
     subprocess.run(["rm", "-rf", d])
