@@ -408,40 +408,65 @@ def e2e_leg(host_data, cs, dev, world):
     With world > 1 every rank runs each pass at the same moment (a barrier
     before each), so the aggregate world x bytes / slowest rank is what N GPUs
     pull over their links and host DRAM together.  Best of 3 passes per route,
-    after one untimed pass that sizes the context's pinned staging."""
+    after one untimed pass that sizes the context's pinned staging.
+
+    A failure on this rank (its context, a pass, the registration) is kept in
+    `error` and never raised: the rank still takes part in every collective
+    (a failed pass reports an infinite time, so the aggregate reads 0), so the
+    other ranks finish and the line -- whose device-resident `value` was
+    measured before this leg -- is still printed."""
     from bitflood_amd import ChunkHasher, chunk_table
     offs, sizes = chunk_table(host_data.size, cs)
     gib = host_data.size / GIB
+    err = []
+
+    def attempt(fn, what):
+        if err:
+            return None
+        try:
+            return fn()
+        except Exception as e:  # recorded, see above
+            err.append(f"{what}: {type(e).__name__}: {e}")
+            return None
 
     def passes(h, k=3):
         best_agg, best_own, d = 0.0, float("inf"), None
         for _ in range(k):
             barrier(world)
             t0 = time.perf_counter()
-            d = h.hash_chunks(host_data, offs, sizes)
-            t = time.perf_counter() - t0
+            d = attempt(lambda: h.hash_chunks(host_data, offs, sizes), "hash pass")
+            t = time.perf_counter() - t0 if not err else float("inf")
             t_max = max_over_ranks(t, world)
             best_agg = max(best_agg, world * gib / t_max)
             best_own = min(best_own, t)
         return best_agg, gib / best_own, d
 
-    with ChunkHasher(device_mask=1 << dev) as h:
-        h.hash_chunks(host_data, offs, sizes)  # warm: sizes the staging to this job
+    h = attempt(lambda: ChunkHasher(device_mask=1 << dev), "lbf_ctx_create")
+    placement = {"device": dev, "numa_node": -1, "staging_node": -1, "bound_cpus": 0}
+    reg_s, s0, s1, registered = 0.0, {"direct": 0}, {"direct": 0}, False
+    try:
+        attempt(lambda: h.hash_chunks(host_data, offs, sizes), "warm pass")  # sizes the staging to this job
         pag_agg, pag_own, d_pag = passes(h)
-        placement = h.worker_info(0)
+        placement = attempt(lambda: h.worker_info(0), "worker_info") or placement
         t0 = time.perf_counter()
-        h.register_host(host_data)
+        registered = attempt(lambda: h.register_host(host_data) or True, "lbf_host_register") or False
         reg_s = time.perf_counter() - t0
-        s0 = h.staging_stats()
-        try:
-            reg_agg, reg_own, d_reg = passes(h)
-            s1 = h.staging_stats()
-        finally:
-            h.unregister_host(host_data)
+        s0 = attempt(lambda: h.staging_stats(), "staging_stats") or s0
+        reg_agg, reg_own, d_reg = passes(h)
+        s1 = attempt(lambda: h.staging_stats(), "staging_stats") or s1
+    finally:
+        if h is not None:
+            if registered:
+                try:
+                    h.unregister_host(host_data)
+                except Exception as e:
+                    err.append(f"lbf_host_unregister: {type(e).__name__}: {e}")
+            h.close()
     return {"pageable_agg": pag_agg, "pageable_own": pag_own, "registered_agg": reg_agg,
             "registered_own": reg_own, "register_s": reg_s,
             "direct_fraction": (s1["direct"] - s0["direct"]) / max(1, 3 * host_data.size),
-            "digests": d_pag, "registered_equal": bool(np.array_equal(d_reg, d_pag)), "placement": placement}
+            "digests": d_pag, "registered_equal": d_reg is not None and bool(np.array_equal(d_reg, d_pag)),
+            "placement": placement, "error": err[0] if err else None}
 
 
 def inproc_leg(buf, slice_bytes, cs, shard_starts, slice_hashes):
@@ -706,6 +731,9 @@ def main():
                 gather_ints(r["placement"]["staging_node"], world))],
         }
         e2e_multi["parity"] = all(x == 1 for x in e2e_multi["parity_per_rank"])
+        e2e_multi["failed_per_rank"] = gather_ints(r["error"] is not None, world)
+        if r["error"]:
+            e2e_multi["error_rank0"] = r["error"]
     slice_hashes = gather_ints(slice_hash(digests[:n_slice]), world)
     shard_starts = [shard_range(world * n_chunks, q, world)[0] * cs for q in range(world)]
 
@@ -807,6 +835,8 @@ def main():
                 out["e2e_registered"] = {"gibs": round(r["registered_own"], 3), "register_s": round(r["register_s"], 4),
                                          "direct_fraction": round(r["direct_fraction"], 4),
                                          "parity": r["registered_equal"]}
+                if r["error"]:
+                    out["e2e_error"] = r["error"]
                 cb["host"]["gpu0_numa_node"] = r["placement"]["numa_node"]
         out["first_chunk_b64"] = b64_27(bytes(digests[0]))
     if world > 1:
