@@ -633,5 +633,167 @@ __global__ void __launch_bounds__(192) sha1_pc4_kernel(ChunkParams p) {
 #undef PC4_ACC
 }
 
+// ---------------------------------------------------------------------------
+// Kernel "pc4x2" (variant 12): two pc4 groups in one 6-wave workgroup, for
+// 16 K-32 K chains (C4 per GPU).
+//
+// pcx5 gives each of a CU's two consumers one producer, because the waves of
+// a CU must each own a SIMD; one producer cannot add all 80 round constants
+// and store 20 KiB per step in time, so pcx5's consumers add K themselves in
+// 64 rounds (the two-add3 round, ≈2.65 cycles more each).  Two producers CAN
+// share a SIMD: one wave's LDS stores drain while the other issues its VALU,
+// so two half steps on one SIMD take ≈1,440 cycles against ≈1,045 for one
+// alone (tools/probe_shared_producers.hip).  Waves k and k+4 of a workgroup
+// land on the same SIMD, so here waves 2 and 3 are the two consumers, each
+// alone on its SIMD, and waves 0, 1 (group 0) and 4, 5 (group 1) are the
+// producers, two to a SIMD.  Each group is pc4 unchanged (steps alternate
+// between its two producers, the consumer runs W+K rounds and double-buffers
+// the next step in registers), except that the W ring has 3 slots instead of
+// 4 so that both groups fit 160 KiB of LDS: step s goes into slot s % 3 after
+// barrier s-3, and the consumer's loads of step s-3 from that slot were
+// issued in its step s-4 and drained by the s_waitcnt lgkmcnt(0) that opens
+// barrier s-3 (step 0 is loaded before an extra barrier that ends the
+// prologue).  Both groups pass the same barriers, so every wave counts the
+// steps of both groups' chains.  LDS 152 KiB: one workgroup per CU.
+// ---------------------------------------------------------------------------
+constexpr int kPc4x2Ring = 3;
+constexpr int kPc4x2GroupU4 = kPc4x2Ring * kPcSlotU4 + 2 * kP2Raw * kPcRawU4;
+constexpr int kPc4x2LdsBytes = 2 * kPc4x2GroupU4 * 16;
+
+template <int kHalf>
+__device__ __forceinline__ void pc4x2_store_half(uint32_t (&w)[16], uint4* ring, uint32_t step, int lane) {
+#if defined(LBF_X2_DIAG) && LBF_X2_DIAG == 2
+  // diagnostic build (tools/probe_pc.hip): the schedule without its LDS stores
+#pragma unroll
+  for (int i = 16 * kHalf; i < 16 * kHalf + 16; ++i) {
+    w[i & 15] = sched(w[(i + 13) & 15], w[(i + 8) & 15], w[(i + 2) & 15], w[i & 15]) + round_k(i);
+    asm volatile("" ::"v"(w[i & 15]));
+  }
+  (void)ring, (void)step, (void)lane;
+#else
+  expand_store_wk2<kHalf>(w, reinterpret_cast<uint2*>(ring + (step % kPc4x2Ring) * kPcSlotU4) + lane, kPcLanes);
+#endif
+}
+
+template <bool kUniform>
+__global__ void __launch_bounds__(384) sha1_pc4x2_kernel(ChunkParams p) {
+  extern __shared__ __attribute__((aligned(16))) uint4 lds[];  // group 0 | group 1: W[3][20][64] | raw[2][2][4][64]
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = wave < 3 ? 0 : 1;
+  const uint32_t first = blockIdx.x * (2 * kPcLanes);
+  const uint32_t i = first + g * kPcLanes + lane;
+  const ChainInfo c = chain_info<kUniform>(p, i);
+  const uint32_t other = chain_info<kUniform>(p, first + (1 - g) * kPcLanes + lane).total;
+  const uint32_t nsteps = __builtin_amdgcn_readfirstlane(max(wave_max(c.total), wave_max(other)));
+  uint4* ring = lds + g * kPc4x2GroupU4;
+#ifdef LBF_PC_STAMPS
+  unsigned long long acc[4] = {0, 0, 0, 0}, t0 = 0, t1 = 0, t2 = 0;
+#define PC4_ACC , acc
+#else
+#define PC4_ACC
+#endif
+#if defined(LBF_X2_DIAG) && LBF_X2_DIAG == 1
+  // diagnostic build (tools/probe_pc.hip): group 1 only passes the barriers
+  if (g == 1) {
+    for (uint32_t b = 0; b < nsteps + (nsteps > 0); ++b) __syncthreads();
+    return;
+  }
+#endif
+
+  if (wave != 2 && wave != 3) {
+    // ---------------- producer X of group g: steps X, X+2, ... ----------------
+    const uint32_t X = g == 0 ? wave : wave - 4;
+    uint4* raw = ring + kPc4x2Ring * kPcSlotU4 + X * (kP2Raw * kPcRawU4);
+    const uint32_t raw_lds = (uint32_t)reinterpret_cast<uintptr_t>(raw);
+    p2_dma(c, X, raw_lds, 0);
+    p2_dma(c, X + 2, raw_lds, 1);
+    uint32_t w[16];
+    auto first_half = [&](uint32_t step) {
+      const uint32_t j = (step - X) >> 1;
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // block j landed; only j+1's DMAs pending
+      p2_block(w, raw + (j & 1u) * kPcRawU4 + lane, c, step);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // raw slot read before it is refilled
+      p2_dma(c, step + 4, raw_lds, j & 1u);
+      pc4x2_store_half<0>(w, ring, step, lane);
+    };
+    if (nsteps > 0) {
+      // prologue: step X whole, then barrier E (see the consumer)
+      if (X < nsteps) {
+        first_half(X);
+        pc4x2_store_half<1>(w, ring, X, lane);
+      }
+      PC4_SYNC();  // barrier E: steps 0 and 1 complete
+    }
+    for (uint32_t b = 0; b < nsteps; ++b) {
+      PC_STAMP(t0);
+      const uint32_t fin = b + 1;  // finished in interval b by producer fin % 2 (step 1: in the prologue)
+      if ((fin & 1u) == X && fin < nsteps && b > 0) pc4x2_store_half<1>(w, ring, fin, lane);
+      const uint32_t start = b + 2;  // started in interval b by producer start % 2
+      if ((start & 1u) == X && start < nsteps) first_half(start);
+      PC_STAMP(t1);
+      PC4_SYNC();  // barrier b: steps <= b + 1 complete
+      PC_STAMP(t2);
+      PC_ACC(1, t0, t1);
+      PC_ACC(2, t1, t2);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA outlives the workgroup
+  } else {
+    // ---------------- consumer of group g ----------------
+    Digest s;
+    s.init();
+    Pc4Sched<2> A, B;
+    const uint32_t min_steps =
+        __builtin_amdgcn_readfirstlane(wave_min(i < p.n ? c.total : 0xFFFFFFFFu));
+    if (nsteps > 0) {
+      // With 3 slots, step 3's first half goes into slot 0 in interval 1, so
+      // step 0 must be loaded out of slot 0 before barrier 0: an extra barrier
+      // E ends the prologue, in which the producers build steps 0 and 1 whole.
+      PC4_SYNC();  // barrier E: steps 0 and 1 complete
+      A.load_all(Pc4Sched<2>::col(ring, 0, lane));
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): slot 0 is free from barrier 0 on
+      pc4_barrier(s PC4_ACC);  // barrier 0
+    }
+    uint32_t k = 0;
+    // Six steps per iteration (the A/B register sets and the 3-slot ring both
+    // come back to where they started), slots as compile-time offsets.
+    const uint32_t fast_end = __builtin_amdgcn_readfirstlane(nsteps ? min(min_steps, nsteps - 1) : 0u);
+    for (; k + 6 <= fast_end; k += 6) {
+      pc4_step(s, A, B, Pc4Sched<2>::col(ring, 1, lane), true, true);
+      pc4_barrier(s PC4_ACC);  // barrier k+1
+      pc4_step(s, B, A, Pc4Sched<2>::col(ring, 2, lane), true, true);
+      pc4_barrier(s PC4_ACC);  // barrier k+2
+      pc4_step(s, A, B, Pc4Sched<2>::col(ring, 0, lane), true, true);
+      pc4_barrier(s PC4_ACC);  // barrier k+3
+      pc4_step(s, B, A, Pc4Sched<2>::col(ring, 1, lane), true, true);
+      pc4_barrier(s PC4_ACC);  // barrier k+4
+      pc4_step(s, A, B, Pc4Sched<2>::col(ring, 2, lane), true, true);
+      pc4_barrier(s PC4_ACC);  // barrier k+5
+      pc4_step(s, B, A, Pc4Sched<2>::col(ring, 0, lane), true, true);
+      pc4_barrier(s PC4_ACC);  // barrier k+6
+    }
+    for (; k < nsteps; k += 2) {
+      // after barrier k: steps <= k+1 complete; A holds step k
+      pc4_step(s, A, B, Pc4Sched<2>::col(ring, (k + 1) % kPc4x2Ring, lane), k < c.total, k < min_steps);
+      if (k + 1 >= nsteps) break;
+      pc4_barrier(s PC4_ACC);  // barrier k+1
+      pc4_step(s, B, A, Pc4Sched<2>::col(ring, (k + 2) % kPc4x2Ring, lane), k + 1 < c.total, k + 1 < min_steps);
+      if (k + 2 >= nsteps) break;
+      pc4_barrier(s PC4_ACC);  // barrier k+2
+    }
+    if (i < p.n) write_result(p, i, s);
+  }
+#ifdef LBF_PC_STAMPS
+  if (lane == 0) {
+    unsigned long long* o = g_pc_stamps + (blockIdx.x * 6 + wave) * 4;
+    o[0] = acc[0];
+    o[1] = acc[1];
+    o[2] = acc[2];
+    o[3] = nsteps;
+  }
+#endif
+#undef PC4_ACC
+}
+
 }  // namespace
 }  // namespace lbf

@@ -123,6 +123,17 @@ void launch_pc4(const ChunkParams& p, hipStream_t stream, int kvec) {
 }
 
 template <bool kUniform>
+void launch_pc4x2(const ChunkParams& p, hipStream_t stream) {
+  static std::once_flag once;
+  std::call_once(once, [] {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4x2_kernel<kUniform>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, kPc4x2LdsBytes);
+  });
+  hipLaunchKernelGGL(sha1_pc4x2_kernel<kUniform>, dim3((p.n + 2 * kPcLanes - 1) / (2 * kPcLanes)), dim3(384),
+                     kPc4x2LdsBytes, stream, p);
+}
+
+template <bool kUniform>
 void launch_lds2(const ChunkParams& p, hipStream_t stream) {
   static std::once_flag once;
   std::call_once(once, [] {
@@ -203,6 +214,9 @@ int launch_chunks(const ChunkParams& p, hipStream_t stream) {
     else launch_pc4<false>(p, stream, 2);
   } else if (variant == 10) {
     launch_pcx5<kPx5KFrom>(p, stream);
+  } else if (variant == 12) {
+    if (uniform) launch_pc4x2<true>(p, stream);
+    else launch_pc4x2<false>(p, stream);
   } else if (variant == 11) {
     if (uniform) launch_lds2<true>(p, stream);
     else launch_lds2<false>(p, stream);
@@ -272,11 +286,11 @@ extern "C" int lbf_sha1_uniform_launch(const uint8_t* d_base, uint64_t len, uint
 
 extern "C" int lbf_set_kernel_variant(int variant) {
 #ifdef LBF_EXPERIMENTAL_VARIANTS
-  const bool known = variant >= 0 && variant <= 11;
+  const bool known = variant >= 0 && variant <= 12;
 #else
-  const bool known = variant == 0 || variant == 1 || variant == 7 || variant == 10 || variant == 11;
+  const bool known = variant == 0 || variant == 1 || variant == 7 || variant == 10 || variant == 11 || variant == 12;
 #endif
-  if (!known) return fail(LBF_ERR_INVALID, "unknown kernel variant (shipped: 0 auto, 1, 7, 10, 11)");
+  if (!known) return fail(LBF_ERR_INVALID, "unknown kernel variant (shipped: 0 auto, 1, 7, 10, 11, 12)");
   lbf::g_variant.store(variant);
   return LBF_OK;
 }

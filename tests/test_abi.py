@@ -76,13 +76,13 @@ def test_no_gpu_fails_loudly():
 
 
 def test_shipped_kernel_variants_only():
-    """The product library carries the four shipped kernels (1 lane, 7 pc4/b64,
-    10 pcx5, 11 lds2); the superseded ones exist only in the experimental build."""
+    """The product library carries the five shipped kernels (1 lane, 7 pc4/b64,
+    10 pcx5, 11 lds2, 12 pc4x2); the superseded ones exist only in the experimental build."""
     lib = _capi.load()
     try:
-        for v in (0, 1, 7, 10, 11):
+        for v in (0, 1, 7, 10, 11, 12):
             assert lib.lbf_set_kernel_variant(v) == _capi.LBF_OK, v
-        for v in (2, 3, 4, 5, 6, 8, 9, 12, -1):
+        for v in (2, 3, 4, 5, 6, 8, 9, 13, -1):
             assert lib.lbf_set_kernel_variant(v) == _capi.LBF_ERR_INVALID, v
         # automatic choice by chain count (DESIGN.md §4.4)
         lib.lbf_set_kernel_variant(0)

@@ -28,10 +28,10 @@ SEED_C = 0x5EED
 # 16-32 K chains), 11 = one chunk per lane with LDS-DMA staging of whole
 # 128-byte lines ("lds2", many chains).  The superseded variants live only in
 # the experimental build (make -C bitflood_amd/csrc experimental).
-VARIANTS = [1, 7, 10, 11]
+VARIANTS = [1, 7, 10, 11, 12]
 
 
-@pytest.fixture(params=VARIANTS, ids=lambda v: {1: "lane", 7: "pc4b64", 10: "pcx5", 11: "lds2"}[v])
+@pytest.fixture(params=VARIANTS, ids=lambda v: {1: "lane", 7: "pc4b64", 10: "pcx5", 11: "lds2", 12: "pc4x2"}[v])
 def variant(request):
     H.set_kernel_variant(request.param)
     yield request.param

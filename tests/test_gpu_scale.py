@@ -20,7 +20,7 @@ pytestmark = pytest.mark.gpu
 GIB = 1 << 30
 
 
-@pytest.fixture(params=[0, 1, 7, 10, 11], ids=["auto", "lane", "pc4b64", "pcx5", "lds2"])
+@pytest.fixture(params=[0, 1, 7, 10, 11, 12], ids=["auto", "lane", "pc4b64", "pcx5", "lds2", "pc4x2"])
 def variant(request):
     H.set_kernel_variant(request.param)
     yield request.param
@@ -95,7 +95,7 @@ def test_c4_all_shards(golden):
         for sh in c4["shards"]:
             assert sh["n_chunks"] == n
             buf.fill_synthetic(c4["seed"], start=sh["first_chunk"] * cs)
-            for v in ([0, 1, 7, 11] if sh["rank"] == 5 else [0]):
+            for v in ([0, 1, 7, 10, 11, 12] if sh["rank"] == 5 else [0]):
                 H.set_kernel_variant(v)
                 H.uniform_launch(buf, shard_bytes, cs, 0, n, dig)
                 H.synchronize()

@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--max-gib", type=int, default=64)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--variants", default="1,7,10,11")
+    ap.add_argument("--points", default="", help="chunk_size:count,... instead of the built-in list")
     a = ap.parse_args()
     size = a.max_gib * GIB
     buf = DeviceBuffer(size)
@@ -44,6 +45,8 @@ def main():
     points = [(262144, n) for n in (4096, 8192, 16384, 32768, 65536, 131072, 262144)]
     points += [(1 << 20, n) for n in (8192, 16384, 32768, 65536)]
     points += [(65536, n) for n in (16384, 65536, 262144, 1048576)]
+    if a.points:
+        points = [tuple(int(x) for x in pt.split(":")) for pt in a.points.split(",")]
     for cs, n in points:
         if n * cs > size:
             continue
