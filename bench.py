@@ -60,9 +60,9 @@ KERNELS = {1: "sha1_lane_kernel<true>", 2: "sha1_pc_kernel<true, 2>", 3: "sha1_l
            4: "sha1_pc2_kernel<true>", 5: "sha1_pc_kernel<true, 2, 2>",
            6: "sha1_pc4_kernel<true, 4>", 7: "sha1_pc4_kernel<true, 2>", 8: "sha1_pc4_kernel<true, 1>",
            9: "sha1_pcx4_kernel<true, 40>", 10: "sha1_pcx5_kernel<true, 64>",
-           11: "sha1_lds2_kernel<true>"}
+           11: "sha1_lds2_kernel<true>", 12: "sha1_pc4x2_kernel<true>"}
 # Issue floors per 64-byte block (tools/gen_round_order.py, tools/probe_lds_lanes.hip):
-#  pc2/pc4 consumer: 80 rounds x 5 VALU at one issue per 4.09 cycles -- the chain's own
+#  pc2/pc4/pc4x2 consumer: 80 rounds x 5 VALU at one issue per 4.09 cycles -- the chain's own
 #    arithmetic alone (its 20 schedule loads and the barrier are not counted)
 #  pc/pcx2 consumer: the two-add3 round form with K in a VGPR (23.2 cycles per round measured)
 #  fused lane/lds: 613 VALU; a lone wave issues one per 4.09 cycles, a SIMD retires one per 4
@@ -386,7 +386,7 @@ def compute_floor_ms(variant, cs, n_chunks):
     """Lower bound on one launch from instruction issue alone (SHA-1 is a serial
     chain per chunk, so few chunks are bound by one chain's issue rate)."""
     blocks = (cs + 9 + 63) // 64  # compressions per chunk incl. padding
-    if variant in (4, 6, 7, 8):
+    if variant in (4, 6, 7, 8, 12):
         return blocks * PC2_CYCLES_PER_BLOCK / CLOCK_HZ * 1e3
     if variant in (2, 5):
         return blocks * PC_CYCLES_PER_BLOCK / CLOCK_HZ * 1e3
@@ -794,7 +794,7 @@ def main():
             # SHA-1 is integer VALU work on a serial chain per chunk: the binding
             # limit is instruction issue, not HBM.
             "compute_floor": {
-                "bound": "per-chain issue" if variant in (2, 4, 5, 6, 7, 8, 9, 10) else "valu",
+                "bound": "per-chain issue" if variant in (2, 4, 5, 6, 7, 8, 9, 10, 12) else "valu",
                 "floor_ms": round(floor_ms, 4),
                 "frac": round(floor_ms / (launch_s * 1e3), 4),
                 "clock_ghz": CLOCK_HZ / 1e9,

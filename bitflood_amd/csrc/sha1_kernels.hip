@@ -12,9 +12,11 @@
 //   "pc4/b64" (variant 7): one consumer + two producer waves per 64 chains, the
 //     W+K schedule handed over in LDS and double-buffered in the consumer's
 //     registers as 8-byte pairs -- few chains (<= 16 K, C2).
+//   "pc4x2" (variant 12): two pc4 groups per CU in one 6-wave workgroup, the
+//     producers two to a SIMD -- the 16 K-32 K chain kernel since round 3.
 //   "pcx5" (variant 10): two consumer/producer pairs per CU, K split between
-//     them, words 0..15 read by the consumer from the raw block -- 16-32 K
-//     chains (C4 per GPU).
+//     them, words 0..15 read by the consumer from the raw block -- the 16-32 K
+//     chain kernel (C4 per GPU) until round 3, kept for A/B.
 //   "lds2" (variant 11): one chunk per lane with LDS-DMA staging of whole
 //     128-byte lines -- many chains (C3).
 // The superseded variants (2 pc, 3 lds, 4 pc2, 5 pcx2, 6 pc4/uint4, 8 pc4/b64
@@ -90,7 +92,11 @@ int pick_variant(uint64_t n) {
     // per-block DMA of 3 at C3, traffic 1.14 -> 1.001 x, sweep_v3_v11_lds2.log).
     // Crossovers from tools/sweep_variants.py (profiles/r01/sweep_v123.log,
     // sweep_v245.log, sweep_v46_pc4.log).
-    variant = n <= kPc4MaxChains ? 7 : (n <= kPcMaxChains ? 10 : 11);
+    // Since round 3, 16 K-32 K chains go to pc4x2 (12): two pc4 groups per CU,
+    // their producers two to a SIMD.  Level with or ahead of pcx5 at every
+    // count measured, and far ahead on ragged counts (20,000 chains: 3.45
+    // against 4.83 ms at 256 KiB; profiles/r03/pc4x2/).
+    variant = n <= kPc4MaxChains ? 7 : (n <= kPcMaxChains ? 12 : 11);
   }
   return variant;
 }

@@ -86,7 +86,7 @@ def test_shipped_kernel_variants_only():
             assert lib.lbf_set_kernel_variant(v) == _capi.LBF_ERR_INVALID, v
         # automatic choice by chain count
         lib.lbf_set_kernel_variant(0)
-        assert [lib.lbf_kernel_for(n) for n in (1, 16384, 16385, 32768, 32769, 1 << 20)] == [7, 7, 10, 10, 11, 11]
+        assert [lib.lbf_kernel_for(n) for n in (1, 16384, 16385, 32768, 32769, 1 << 20)] == [7, 7, 12, 12, 11, 11]
     finally:
         lib.lbf_set_kernel_variant(0)
 

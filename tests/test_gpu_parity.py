@@ -25,8 +25,10 @@ SEED_C = 0x5EED
 # per 64 chains with the W+K schedule double-buffered in registers as 8-byte
 # pairs ("pc4b64", <= 16 K chains), 10 = two consumer/producer pairs per CU
 # with the round constants split and words 0..15 from the raw block ("pcx5",
-# 16-32 K chains), 11 = one chunk per lane with LDS-DMA staging of whole
-# 128-byte lines ("lds2", many chains).  The superseded variants live only in
+# 16-32 K chains until round 3), 11 = one chunk per lane with LDS-DMA staging
+# of whole 128-byte lines ("lds2", many chains), 12 = two pc4 groups in one
+# 6-wave workgroup, producers two to a SIMD ("pc4x2", 16-32 K chains since
+# round 3).  The superseded variants live only in
 # the experimental build (make -C bitflood_amd/csrc experimental).
 VARIANTS = [1, 7, 10, 11, 12]
 

@@ -83,7 +83,7 @@ def test_c3_verify_flags_corruption(c3_buffer):
 
 
 def test_c4_all_shards(golden):
-    """Every 32 GiB shard of the 256 GiB C4 file (automatic kernel choice: pcx5
+    """Every 32 GiB shard of the 256 GiB C4 file (automatic kernel choice: pc4x2
     at 32,768 chunks), plus one shard through the other kernels."""
     c4 = golden("c4.json")
     cs = c4["chunk_size"]
