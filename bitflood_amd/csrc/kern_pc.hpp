@@ -525,7 +525,10 @@ __device__ __forceinline__ void pc4_barrier(Digest& s PC4_ACC_ARGS) {
   asm volatile("" : "+v"(s.h[0]), "+v"(s.h[1]), "+v"(s.h[2]), "+v"(s.h[3]), "+v"(s.h[4])::"memory");
 }
 
-template <bool kUniform, int kVec>
+// kUnroll: steps per fast-loop iteration.  Eight since round 3: 0.3-1.1 %
+// faster than four at C2 in alternating runs (profiles/r03/pc4x2/session16/);
+// four is experimental variant 16, for A/B.
+template <bool kUniform, int kVec, int kUnroll = 8>
 __global__ void __launch_bounds__(192) sha1_pc4_kernel(ChunkParams p) {
   extern __shared__ __attribute__((aligned(16))) uint4 ring[];  // W[3][20][64] | raw[2][2][4][64]
   const int lane = threadIdx.x & 63;
@@ -600,7 +603,7 @@ __global__ void __launch_bounds__(192) sha1_pc4_kernel(ChunkParams p) {
     // conditions are folded into one bound, so the loop test is one scalar
     // compare (the compiler built the conjunction from 7 scalar ops).
     const uint32_t fast_end = __builtin_amdgcn_readfirstlane(nsteps ? min(min_steps, nsteps - 1) : 0u);
-    for (; k + 4 <= fast_end; k += 4) {
+    for (; k + kUnroll <= fast_end; k += kUnroll) {
       pc4_step(s, A, B, Pc4Sched<kVec>::col(ring, 1, lane), true, true);
       pc4_barrier(s PC4_ACC);  // barrier k+1
       pc4_step(s, B, A, Pc4Sched<kVec>::col(ring, 2, lane), true, true);
@@ -609,6 +612,16 @@ __global__ void __launch_bounds__(192) sha1_pc4_kernel(ChunkParams p) {
       pc4_barrier(s PC4_ACC);  // barrier k+3
       pc4_step(s, B, A, Pc4Sched<kVec>::col(ring, 0, lane), true, true);
       pc4_barrier(s PC4_ACC);  // barrier k+4
+      if (kUnroll == 8) {
+        pc4_step(s, A, B, Pc4Sched<kVec>::col(ring, 1, lane), true, true);
+        pc4_barrier(s PC4_ACC);  // barrier k+5
+        pc4_step(s, B, A, Pc4Sched<kVec>::col(ring, 2, lane), true, true);
+        pc4_barrier(s PC4_ACC);  // barrier k+6
+        pc4_step(s, A, B, Pc4Sched<kVec>::col(ring, 3, lane), true, true);
+        pc4_barrier(s PC4_ACC);  // barrier k+7
+        pc4_step(s, B, A, Pc4Sched<kVec>::col(ring, 0, lane), true, true);
+        pc4_barrier(s PC4_ACC);  // barrier k+8
+      }
     }
     for (; k < nsteps; k += 2) {
       // after barrier k: steps <= k+1 complete; A holds step k
@@ -671,20 +684,34 @@ __device__ __forceinline__ void pc4x2_store_half(uint32_t (&w)[16], uint4* ring,
   }
   (void)ring, (void)step, (void)lane;
 #else
-  expand_store_wk2<kHalf>(w, reinterpret_cast<uint2*>(ring + (step % kPc4x2Ring) * kPcSlotU4) + lane, kPcLanes);
+  // The slot's byte offset goes through an empty asm: folded into the lane's
+  // address, the compiler addressed the words with negative offsets from a
+  // shifted base and left every store unpaired (40 ds_write_b64 per step
+  // instead of 20 ds_write2st64_b64), which slowed the consumers' reads by 6 %
+  // (C2 with one group, experimental variant 13).
+  uint32_t slot_off = (step % kPc4x2Ring) * (kPcSlotU4 * 16);
+  asm volatile("" : "+s"(slot_off));
+  expand_store_wk2<kHalf>(w, reinterpret_cast<uint2*>(reinterpret_cast<char*>(ring) + slot_off) + lane, kPcLanes);
 #endif
 }
 
-template <bool kUniform>
-__global__ void __launch_bounds__(384) sha1_pc4x2_kernel(ChunkParams p) {
+// kGroups = 1 (experimental variant 13, a diagnostic): one group of three
+// waves, 64 chains per workgroup -- pc4 with pc4x2's 3-slot ring and six-step
+// loop, to tell the cost of that structure from the cost of a second group.
+// kFast = false (experimental variants 14, 15, diagnostics): no six-step loop,
+// every step through the generic two-step loop with runtime slot offsets.
+// kRawAt (experimental variant 17, a diagnostic): where the raw slots start, in
+// W slots from the group's base (pc4's layout has them at 4).
+template <bool kUniform, int kGroups = 2, bool kFast = true, int kRawAt = kPc4x2Ring>
+__global__ void __launch_bounds__(192 * kGroups) sha1_pc4x2_kernel(ChunkParams p) {
   extern __shared__ __attribute__((aligned(16))) uint4 lds[];  // group 0 | group 1: W[3][20][64] | raw[2][2][4][64]
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g = wave < 3 ? 0 : 1;
-  const uint32_t first = blockIdx.x * (2 * kPcLanes);
+  const uint32_t first = blockIdx.x * (kGroups * kPcLanes);
   const uint32_t i = first + g * kPcLanes + lane;
   const ChainInfo c = chain_info<kUniform>(p, i);
-  const uint32_t other = chain_info<kUniform>(p, first + (1 - g) * kPcLanes + lane).total;
+  const uint32_t other = kGroups == 2 ? chain_info<kUniform>(p, first + (1 - g) * kPcLanes + lane).total : 0u;
   const uint32_t nsteps = __builtin_amdgcn_readfirstlane(max(wave_max(c.total), wave_max(other)));
   uint4* ring = lds + g * kPc4x2GroupU4;
 #ifdef LBF_PC_STAMPS
@@ -704,7 +731,7 @@ __global__ void __launch_bounds__(384) sha1_pc4x2_kernel(ChunkParams p) {
   if (wave != 2 && wave != 3) {
     // ---------------- producer X of group g: steps X, X+2, ... ----------------
     const uint32_t X = g == 0 ? wave : wave - 4;
-    uint4* raw = ring + kPc4x2Ring * kPcSlotU4 + X * (kP2Raw * kPcRawU4);
+    uint4* raw = ring + kRawAt * kPcSlotU4 + X * (kP2Raw * kPcRawU4);
     const uint32_t raw_lds = (uint32_t)reinterpret_cast<uintptr_t>(raw);
     p2_dma(c, X, raw_lds, 0);
     p2_dma(c, X + 2, raw_lds, 1);
@@ -757,7 +784,7 @@ __global__ void __launch_bounds__(384) sha1_pc4x2_kernel(ChunkParams p) {
     uint32_t k = 0;
     // Six steps per iteration (the A/B register sets and the 3-slot ring both
     // come back to where they started), slots as compile-time offsets.
-    const uint32_t fast_end = __builtin_amdgcn_readfirstlane(nsteps ? min(min_steps, nsteps - 1) : 0u);
+    const uint32_t fast_end = __builtin_amdgcn_readfirstlane(nsteps && kFast ? min(min_steps, nsteps - 1) : 0u);
     for (; k + 6 <= fast_end; k += 6) {
       pc4_step(s, A, B, Pc4Sched<2>::col(ring, 1, lane), true, true);
       pc4_barrier(s PC4_ACC);  // barrier k+1

@@ -193,6 +193,63 @@ bool launch_experimental(int variant, const ChunkParams& p, hipStream_t stream) 
     else launch_pc4<true>(p, stream, kvec);
   } else if (variant == 9) {
     launch_pcx4<kPx4KFrom>(p, stream);
+  } else if (variant == 13 || variant == 14) {
+    // pc4x2's structure with one group (diagnostics; 14 without the six-step
+    // loop); 100 KiB pins one workgroup per CU
+    constexpr int lds = 100 * 1024;
+    static std::once_flag once;
+    std::call_once(once, [] {
+      for (const void* f : {reinterpret_cast<const void*>(&sha1_pc4x2_kernel<false, 1>),
+                            reinterpret_cast<const void*>(&sha1_pc4x2_kernel<true, 1>),
+                            reinterpret_cast<const void*>(&sha1_pc4x2_kernel<false, 1, false>),
+                            reinterpret_cast<const void*>(&sha1_pc4x2_kernel<true, 1, false>)})
+        (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    });
+    const uint32_t blocks = (p.n + kPcLanes - 1) / kPcLanes;
+    if (variant == 13) {
+      if (p.offsets) hipLaunchKernelGGL((sha1_pc4x2_kernel<false, 1>), dim3(blocks), dim3(192), lds, stream, p);
+      else hipLaunchKernelGGL((sha1_pc4x2_kernel<true, 1>), dim3(blocks), dim3(192), lds, stream, p);
+    } else {
+      if (p.offsets) hipLaunchKernelGGL((sha1_pc4x2_kernel<false, 1, false>), dim3(blocks), dim3(192), lds, stream, p);
+      else hipLaunchKernelGGL((sha1_pc4x2_kernel<true, 1, false>), dim3(blocks), dim3(192), lds, stream, p);
+    }
+  } else if (variant == 16) {
+    // pc4 with its fast loop unrolled by four, the form before round 3 (A/B)
+    static std::once_flag once;
+    std::call_once(once, [] {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4_kernel<false, 2, 4>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, kPc4LdsBytes);
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4_kernel<true, 2, 4>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, kPc4LdsBytes);
+    });
+    const dim3 g((p.n + kPcLanes - 1) / kPcLanes), b(192);
+    if (p.offsets) hipLaunchKernelGGL((sha1_pc4_kernel<false, 2, 4>), g, b, kPc4LdsBytes, stream, p);
+    else hipLaunchKernelGGL((sha1_pc4_kernel<true, 2, 4>), g, b, kPc4LdsBytes, stream, p);
+  } else if (variant == 17) {
+    // variant 13 with pc4's LDS layout: raw slots after four W slots (diagnostic)
+    constexpr int lds = 100 * 1024;
+    static std::once_flag once;
+    std::call_once(once, [] {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4x2_kernel<false, 1, true, 4>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4x2_kernel<true, 1, true, 4>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    });
+    const uint32_t blocks = (p.n + kPcLanes - 1) / kPcLanes;
+    if (p.offsets) hipLaunchKernelGGL((sha1_pc4x2_kernel<false, 1, true, 4>), dim3(blocks), dim3(192), lds, stream, p);
+    else hipLaunchKernelGGL((sha1_pc4x2_kernel<true, 1, true, 4>), dim3(blocks), dim3(192), lds, stream, p);
+  } else if (variant == 15) {
+    // pc4x2 without the six-step loop (diagnostic)
+    static std::once_flag once;
+    std::call_once(once, [] {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4x2_kernel<false, 2, false>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, kPc4x2LdsBytes);
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4x2_kernel<true, 2, false>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, kPc4x2LdsBytes);
+    });
+    const uint32_t blocks = (p.n + 2 * kPcLanes - 1) / (2 * kPcLanes);
+    if (p.offsets) hipLaunchKernelGGL((sha1_pc4x2_kernel<false, 2, false>), dim3(blocks), dim3(384), kPc4x2LdsBytes, stream, p);
+    else hipLaunchKernelGGL((sha1_pc4x2_kernel<true, 2, false>), dim3(blocks), dim3(384), kPc4x2LdsBytes, stream, p);
   } else if (variant == 3) {
     const uint32_t blocks = (p.n + 255) / 256;
     constexpr int lds = 4 * kLdsStages * kPcRawU4 * 16;
@@ -292,7 +349,7 @@ extern "C" int lbf_sha1_uniform_launch(const uint8_t* d_base, uint64_t len, uint
 
 extern "C" int lbf_set_kernel_variant(int variant) {
 #ifdef LBF_EXPERIMENTAL_VARIANTS
-  const bool known = variant >= 0 && variant <= 12;
+  const bool known = variant >= 0 && variant <= 17;
 #else
   const bool known = variant == 0 || variant == 1 || variant == 7 || variant == 10 || variant == 11 || variant == 12;
 #endif

@@ -20,17 +20,20 @@ static void run(int variant, uint8_t* buf, uint64_t len, uint32_t cs, uint8_t* d
   }
   const bool px = variant == 10;  // two pairs per workgroup: waves 0,1 consume, 2,3 produce
   const bool x2 = variant == 12;   // pc4x2: waves 2,3 consume; 0,4 are producer 0 and 1,5 producer 1 of each group
+  const bool x1 = variant == 13;   // pc4x2's structure, one group: wave 2 consumes, 0 and 1 produce (stamps at wg * 6)
   const int wgs = (int)((n + (px || x2 ? 127 : 63)) / (px || x2 ? 128 : 64));
-  const int nw = (variant == 4 || variant == 6 || variant == 7) ? 3 : px ? 4 : x2 ? 6 : 2;  // waves per workgroup
+  const int nw = (variant == 4 || variant == 6 || variant == 7) ? 3 : px ? 4 : x2 || x1 ? 6 : 2;  // waves per workgroup
   std::vector<unsigned long long> h(wgs * nw * 4);
   hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(lbf::g_pc_stamps), wgs * nw * 4 * 8, 0, hipMemcpyDeviceToHost);
   double a[3][3] = {{0}};
   double steps = 0;
   // roles: 0 = consumer(s), 1.. = producer(s); pcx5's two pairs fold into one consumer and one producer
-  const int roles = px ? 2 : x2 ? 3 : nw;
+  const int roles = px ? 2 : x2 || x1 ? 3 : nw;
   for (int w = 0; w < wgs; ++w)
     for (int r = 0; r < nw; ++r) {
-      const int role = px ? (r >= 2 ? 1 : 0) : x2 ? (r == 2 || r == 3 ? 0 : r == 0 || r == 4 ? 1 : 2) : r;
+      if (x1 && r > 2) continue;
+      const int role = px ? (r >= 2 ? 1 : 0) : x2 ? (r == 2 || r == 3 ? 0 : r == 0 || r == 4 ? 1 : 2)
+                     : x1 ? (r == 2 ? 0 : r + 1) : r;
       for (int j = 0; j < 3; ++j) a[role][j] += (double)h[(w * nw + r) * 4 + j] / (px || x2 ? 2 : 1);
       if (r == 0) steps += (double)h[(w * nw) * 4 + 3];
     }
@@ -60,6 +63,7 @@ int main(int argc, char** argv) {
   run(10, buf, 8ull << 30, 262144, dig);
   run(12, buf, 8ull << 30, 262144, dig);
   run(7, buf, 4ull << 30, 262144, dig);
+  run(13, buf, 4ull << 30, 262144, dig);
   if (all)
     for (int v : {4, 6}) run(v, buf, 4ull << 30, 262144, dig);
   hipFree(buf);
