@@ -526,7 +526,7 @@ __device__ __forceinline__ void pc4_barrier(Digest& s PC4_ACC_ARGS) {
 }
 
 // kUnroll: steps per fast-loop iteration.  Eight since round 3: 0.3-1.1 %
-// faster than four at C2 in alternating runs (profiles/r03/pc4x2/session16/);
+// faster than four at C2 in alternating runs (profiles/r03/pc4x2/diag/sweep_7_16_*.jsonl);
 // four is experimental variant 16, for A/B.
 template <bool kUniform, int kVec, int kUnroll = 8>
 __global__ void __launch_bounds__(192) sha1_pc4_kernel(ChunkParams p) {
