@@ -702,7 +702,9 @@ __device__ __forceinline__ void pc4x2_store_half(uint32_t (&w)[16], uint4* ring,
 // every step through the generic two-step loop with runtime slot offsets.
 // kRawAt (experimental variant 17, a diagnostic): where the raw slots start, in
 // W slots from the group's base (pc4's layout has them at 4).
-template <bool kUniform, int kGroups = 2, bool kFast = true, int kRawAt = kPc4x2Ring>
+// kFence (experimental variants 18, 19, diagnostics): scheduling barriers
+// around the producers' workgroup barrier, as the stamped build has them.
+template <bool kUniform, int kGroups = 2, bool kFast = true, int kRawAt = kPc4x2Ring, bool kFence = false>
 __global__ void __launch_bounds__(192 * kGroups) sha1_pc4x2_kernel(ChunkParams p) {
   extern __shared__ __attribute__((aligned(16))) uint4 lds[];  // group 0 | group 1: W[3][20][64] | raw[2][2][4][64]
   const int lane = threadIdx.x & 63;
@@ -759,7 +761,9 @@ __global__ void __launch_bounds__(192 * kGroups) sha1_pc4x2_kernel(ChunkParams p
       const uint32_t start = b + 2;  // started in interval b by producer start % 2
       if ((start & 1u) == X && start < nsteps) first_half(start);
       PC_STAMP(t1);
+      if (kFence) __builtin_amdgcn_sched_barrier(0);
       PC4_SYNC();  // barrier b: steps <= b + 1 complete
+      if (kFence) __builtin_amdgcn_sched_barrier(0);
       PC_STAMP(t2);
       PC_ACC(1, t0, t1);
       PC_ACC(2, t1, t2);
