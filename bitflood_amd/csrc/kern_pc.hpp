@@ -603,24 +603,14 @@ __global__ void __launch_bounds__(192) sha1_pc4_kernel(ChunkParams p) {
     // conditions are folded into one bound, so the loop test is one scalar
     // compare (the compiler built the conjunction from 7 scalar ops).
     const uint32_t fast_end = __builtin_amdgcn_readfirstlane(nsteps ? min(min_steps, nsteps - 1) : 0u);
+    static_assert(kUnroll % 4 == 0, "the fast loop keeps k % 4 == 0");
     for (; k + kUnroll <= fast_end; k += kUnroll) {
-      pc4_step(s, A, B, Pc4Sched<kVec>::col(ring, 1, lane), true, true);
-      pc4_barrier(s PC4_ACC);  // barrier k+1
-      pc4_step(s, B, A, Pc4Sched<kVec>::col(ring, 2, lane), true, true);
-      pc4_barrier(s PC4_ACC);  // barrier k+2
-      pc4_step(s, A, B, Pc4Sched<kVec>::col(ring, 3, lane), true, true);
-      pc4_barrier(s PC4_ACC);  // barrier k+3
-      pc4_step(s, B, A, Pc4Sched<kVec>::col(ring, 0, lane), true, true);
-      pc4_barrier(s PC4_ACC);  // barrier k+4
-      if (kUnroll == 8) {
-        pc4_step(s, A, B, Pc4Sched<kVec>::col(ring, 1, lane), true, true);
-        pc4_barrier(s PC4_ACC);  // barrier k+5
-        pc4_step(s, B, A, Pc4Sched<kVec>::col(ring, 2, lane), true, true);
-        pc4_barrier(s PC4_ACC);  // barrier k+6
-        pc4_step(s, A, B, Pc4Sched<kVec>::col(ring, 3, lane), true, true);
-        pc4_barrier(s PC4_ACC);  // barrier k+7
-        pc4_step(s, B, A, Pc4Sched<kVec>::col(ring, 0, lane), true, true);
-        pc4_barrier(s PC4_ACC);  // barrier k+8
+#pragma unroll
+      for (int j = 0; j < kUnroll; j += 2) {
+        pc4_step(s, A, B, Pc4Sched<kVec>::col(ring, (j + 1) % 4, lane), true, true);
+        pc4_barrier(s PC4_ACC);  // barrier k+j+1
+        pc4_step(s, B, A, Pc4Sched<kVec>::col(ring, (j + 2) % 4, lane), true, true);
+        pc4_barrier(s PC4_ACC);  // barrier k+j+2
       }
     }
     for (; k < nsteps; k += 2) {

@@ -262,6 +262,18 @@ bool launch_experimental(int variant, const ChunkParams& p, hipStream_t stream) 
       if (p.offsets) hipLaunchKernelGGL((sha1_pc4x2_kernel<false, 1, true, 3, true>), dim3(blocks), dim3(192), lds1, stream, p);
       else hipLaunchKernelGGL((sha1_pc4x2_kernel<true, 1, true, 3, true>), dim3(blocks), dim3(192), lds1, stream, p);
     }
+  } else if (variant == 20) {
+    // pc4 with its fast loop unrolled by sixteen (A/B)
+    static std::once_flag once;
+    std::call_once(once, [] {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4_kernel<false, 2, 16>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, kPc4LdsBytes);
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4_kernel<true, 2, 16>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, kPc4LdsBytes);
+    });
+    const dim3 g((p.n + kPcLanes - 1) / kPcLanes), b(192);
+    if (p.offsets) hipLaunchKernelGGL((sha1_pc4_kernel<false, 2, 16>), g, b, kPc4LdsBytes, stream, p);
+    else hipLaunchKernelGGL((sha1_pc4_kernel<true, 2, 16>), g, b, kPc4LdsBytes, stream, p);
   } else if (variant == 15) {
     // pc4x2 without the six-step loop (diagnostic)
     static std::once_flag once;
@@ -373,7 +385,7 @@ extern "C" int lbf_sha1_uniform_launch(const uint8_t* d_base, uint64_t len, uint
 
 extern "C" int lbf_set_kernel_variant(int variant) {
 #ifdef LBF_EXPERIMENTAL_VARIANTS
-  const bool known = variant >= 0 && variant <= 19;
+  const bool known = variant >= 0 && variant <= 20;
 #else
   const bool known = variant == 0 || variant == 1 || variant == 7 || variant == 10 || variant == 11 || variant == 12;
 #endif
