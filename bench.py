@@ -60,7 +60,7 @@ KERNELS = {1: "sha1_lane_kernel<true>", 2: "sha1_pc_kernel<true, 2>", 3: "sha1_l
            4: "sha1_pc2_kernel<true>", 5: "sha1_pc_kernel<true, 2, 2>",
            6: "sha1_pc4_kernel<true, 4>", 7: "sha1_pc4_kernel<true, 2, 8>", 8: "sha1_pc4_kernel<true, 1>",
            9: "sha1_pcx4_kernel<true, 40>", 10: "sha1_pcx5_kernel<true, 64>",
-           11: "sha1_lds2_kernel<true>", 12: "sha1_pc4x2_kernel<true, 2, true, 3>"}
+           11: "sha1_lds2_kernel<true>", 12: "sha1_pc4x2_kernel<true>"}
 # Issue floors per 64-byte block (tools/gen_round_order.py, tools/probe_lds_lanes.hip):
 #  pc2/pc4/pc4x2 consumer: 80 rounds x 5 VALU at one issue per 4.09 cycles -- the chain's own
 #    arithmetic alone (its 20 schedule loads and the barrier are not counted)

@@ -694,8 +694,10 @@ __device__ __forceinline__ void pc4x2_store_half(uint32_t (&w)[16], uint4* ring,
 // W slots from the group's base (pc4's layout has them at 4).
 // kFence (experimental variants 18, 19, diagnostics): scheduling barriers
 // around the producers' workgroup barrier, as the stamped build has them.
-template <bool kUniform, int kGroups = 2, bool kFast = true, int kRawAt = kPc4x2Ring, bool kFence = false>
-__global__ void __launch_bounds__(192 * kGroups) sha1_pc4x2_kernel(ChunkParams p) {
+// kUnroll6 (a multiple of 6): steps per fast-loop iteration (12: experimental variant 21).
+template <bool kUniform, int kGroups, bool kFast, int kRawAt, bool kFence, int kUnroll6>
+__device__ __forceinline__ void pc4x2_body(const ChunkParams& p) {
+  static_assert(kUnroll6 % 6 == 0, "the fast loop keeps k % 6 == 0");
   extern __shared__ __attribute__((aligned(16))) uint4 lds[];  // group 0 | group 1: W[3][20][64] | raw[2][2][4][64]
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -779,19 +781,14 @@ __global__ void __launch_bounds__(192 * kGroups) sha1_pc4x2_kernel(ChunkParams p
     // Six steps per iteration (the A/B register sets and the 3-slot ring both
     // come back to where they started), slots as compile-time offsets.
     const uint32_t fast_end = __builtin_amdgcn_readfirstlane(nsteps && kFast ? min(min_steps, nsteps - 1) : 0u);
-    for (; k + 6 <= fast_end; k += 6) {
-      pc4_step(s, A, B, Pc4Sched<2>::col(ring, 1, lane), true, true);
-      pc4_barrier(s PC4_ACC);  // barrier k+1
-      pc4_step(s, B, A, Pc4Sched<2>::col(ring, 2, lane), true, true);
-      pc4_barrier(s PC4_ACC);  // barrier k+2
-      pc4_step(s, A, B, Pc4Sched<2>::col(ring, 0, lane), true, true);
-      pc4_barrier(s PC4_ACC);  // barrier k+3
-      pc4_step(s, B, A, Pc4Sched<2>::col(ring, 1, lane), true, true);
-      pc4_barrier(s PC4_ACC);  // barrier k+4
-      pc4_step(s, A, B, Pc4Sched<2>::col(ring, 2, lane), true, true);
-      pc4_barrier(s PC4_ACC);  // barrier k+5
-      pc4_step(s, B, A, Pc4Sched<2>::col(ring, 0, lane), true, true);
-      pc4_barrier(s PC4_ACC);  // barrier k+6
+    for (; k + kUnroll6 <= fast_end; k += kUnroll6) {
+#pragma unroll
+      for (int j = 0; j < kUnroll6; j += 2) {
+        pc4_step(s, A, B, Pc4Sched<2>::col(ring, (j + 1) % kPc4x2Ring, lane), true, true);
+        pc4_barrier(s PC4_ACC);  // barrier k+j+1
+        pc4_step(s, B, A, Pc4Sched<2>::col(ring, (j + 2) % kPc4x2Ring, lane), true, true);
+        pc4_barrier(s PC4_ACC);  // barrier k+j+2
+      }
     }
     for (; k < nsteps; k += 2) {
       // after barrier k: steps <= k+1 complete; A holds step k
@@ -815,6 +812,20 @@ __global__ void __launch_bounds__(192 * kGroups) sha1_pc4x2_kernel(ChunkParams p
 #endif
 #undef PC4_ACC
 }
+
+// The shipped kernel (variant 12).
+template <bool kUniform>
+__global__ void __launch_bounds__(384) sha1_pc4x2_kernel(ChunkParams p) {
+  pc4x2_body<kUniform, 2, true, kPc4x2Ring, false, 6>(p);
+}
+
+#ifdef LBF_EXPERIMENTAL_VARIANTS
+// Diagnostic forms (experimental variants 13-15, 17-19, 21).
+template <bool kUniform, int kGroups, bool kFast, int kRawAt, bool kFence, int kUnroll6>
+__global__ void __launch_bounds__(192 * kGroups) sha1_pc4x2_diag_kernel(ChunkParams p) {
+  pc4x2_body<kUniform, kGroups, kFast, kRawAt, kFence, kUnroll6>(p);
+}
+#endif
 
 }  // namespace
 }  // namespace lbf

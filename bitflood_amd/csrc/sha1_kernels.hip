@@ -199,19 +199,19 @@ bool launch_experimental(int variant, const ChunkParams& p, hipStream_t stream) 
     constexpr int lds = 100 * 1024;
     static std::once_flag once;
     std::call_once(once, [] {
-      for (const void* f : {reinterpret_cast<const void*>(&sha1_pc4x2_kernel<false, 1>),
-                            reinterpret_cast<const void*>(&sha1_pc4x2_kernel<true, 1>),
-                            reinterpret_cast<const void*>(&sha1_pc4x2_kernel<false, 1, false>),
-                            reinterpret_cast<const void*>(&sha1_pc4x2_kernel<true, 1, false>)})
+      for (const void* f : {reinterpret_cast<const void*>(&sha1_pc4x2_diag_kernel<false, 1, true, 3, false, 6>),
+                            reinterpret_cast<const void*>(&sha1_pc4x2_diag_kernel<true, 1, true, 3, false, 6>),
+                            reinterpret_cast<const void*>(&sha1_pc4x2_diag_kernel<false, 1, false, 3, false, 6>),
+                            reinterpret_cast<const void*>(&sha1_pc4x2_diag_kernel<true, 1, false, 3, false, 6>)})
         (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     });
     const uint32_t blocks = (p.n + kPcLanes - 1) / kPcLanes;
     if (variant == 13) {
-      if (p.offsets) hipLaunchKernelGGL((sha1_pc4x2_kernel<false, 1>), dim3(blocks), dim3(192), lds, stream, p);
-      else hipLaunchKernelGGL((sha1_pc4x2_kernel<true, 1>), dim3(blocks), dim3(192), lds, stream, p);
+      if (p.offsets) hipLaunchKernelGGL((sha1_pc4x2_diag_kernel<false, 1, true, 3, false, 6>), dim3(blocks), dim3(192), lds, stream, p);
+      else hipLaunchKernelGGL((sha1_pc4x2_diag_kernel<true, 1, true, 3, false, 6>), dim3(blocks), dim3(192), lds, stream, p);
     } else {
-      if (p.offsets) hipLaunchKernelGGL((sha1_pc4x2_kernel<false, 1, false>), dim3(blocks), dim3(192), lds, stream, p);
-      else hipLaunchKernelGGL((sha1_pc4x2_kernel<true, 1, false>), dim3(blocks), dim3(192), lds, stream, p);
+      if (p.offsets) hipLaunchKernelGGL((sha1_pc4x2_diag_kernel<false, 1, false, 3, false, 6>), dim3(blocks), dim3(192), lds, stream, p);
+      else hipLaunchKernelGGL((sha1_pc4x2_diag_kernel<true, 1, false, 3, false, 6>), dim3(blocks), dim3(192), lds, stream, p);
     }
   } else if (variant == 16) {
     // pc4 with its fast loop unrolled by four, the form before round 3 (A/B)
@@ -230,37 +230,37 @@ bool launch_experimental(int variant, const ChunkParams& p, hipStream_t stream) 
     constexpr int lds = 100 * 1024;
     static std::once_flag once;
     std::call_once(once, [] {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4x2_kernel<false, 1, true, 4>),
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4x2_diag_kernel<false, 1, true, 4, false, 6>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4x2_kernel<true, 1, true, 4>),
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4x2_diag_kernel<true, 1, true, 4, false, 6>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     });
     const uint32_t blocks = (p.n + kPcLanes - 1) / kPcLanes;
-    if (p.offsets) hipLaunchKernelGGL((sha1_pc4x2_kernel<false, 1, true, 4>), dim3(blocks), dim3(192), lds, stream, p);
-    else hipLaunchKernelGGL((sha1_pc4x2_kernel<true, 1, true, 4>), dim3(blocks), dim3(192), lds, stream, p);
+    if (p.offsets) hipLaunchKernelGGL((sha1_pc4x2_diag_kernel<false, 1, true, 4, false, 6>), dim3(blocks), dim3(192), lds, stream, p);
+    else hipLaunchKernelGGL((sha1_pc4x2_diag_kernel<true, 1, true, 4, false, 6>), dim3(blocks), dim3(192), lds, stream, p);
   } else if (variant == 18 || variant == 19) {
     // pc4x2 (18) and its one-group form (19) with scheduling barriers around the
     // producers' workgroup barrier (diagnostics)
     constexpr int lds1 = 100 * 1024;
     static std::once_flag once;
     std::call_once(once, [] {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4x2_kernel<false, 2, true, 3, true>),
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4x2_diag_kernel<false, 2, true, 3, true, 6>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, kPc4x2LdsBytes);
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4x2_kernel<true, 2, true, 3, true>),
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4x2_diag_kernel<true, 2, true, 3, true, 6>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, kPc4x2LdsBytes);
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4x2_kernel<false, 1, true, 3, true>),
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4x2_diag_kernel<false, 1, true, 3, true, 6>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, lds1);
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4x2_kernel<true, 1, true, 3, true>),
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4x2_diag_kernel<true, 1, true, 3, true, 6>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, lds1);
     });
     if (variant == 18) {
       const uint32_t blocks = (p.n + 2 * kPcLanes - 1) / (2 * kPcLanes);
-      if (p.offsets) hipLaunchKernelGGL((sha1_pc4x2_kernel<false, 2, true, 3, true>), dim3(blocks), dim3(384), kPc4x2LdsBytes, stream, p);
-      else hipLaunchKernelGGL((sha1_pc4x2_kernel<true, 2, true, 3, true>), dim3(blocks), dim3(384), kPc4x2LdsBytes, stream, p);
+      if (p.offsets) hipLaunchKernelGGL((sha1_pc4x2_diag_kernel<false, 2, true, 3, true, 6>), dim3(blocks), dim3(384), kPc4x2LdsBytes, stream, p);
+      else hipLaunchKernelGGL((sha1_pc4x2_diag_kernel<true, 2, true, 3, true, 6>), dim3(blocks), dim3(384), kPc4x2LdsBytes, stream, p);
     } else {
       const uint32_t blocks = (p.n + kPcLanes - 1) / kPcLanes;
-      if (p.offsets) hipLaunchKernelGGL((sha1_pc4x2_kernel<false, 1, true, 3, true>), dim3(blocks), dim3(192), lds1, stream, p);
-      else hipLaunchKernelGGL((sha1_pc4x2_kernel<true, 1, true, 3, true>), dim3(blocks), dim3(192), lds1, stream, p);
+      if (p.offsets) hipLaunchKernelGGL((sha1_pc4x2_diag_kernel<false, 1, true, 3, true, 6>), dim3(blocks), dim3(192), lds1, stream, p);
+      else hipLaunchKernelGGL((sha1_pc4x2_diag_kernel<true, 1, true, 3, true, 6>), dim3(blocks), dim3(192), lds1, stream, p);
     }
   } else if (variant == 20) {
     // pc4 with its fast loop unrolled by sixteen (A/B)
@@ -274,18 +274,30 @@ bool launch_experimental(int variant, const ChunkParams& p, hipStream_t stream) 
     const dim3 g((p.n + kPcLanes - 1) / kPcLanes), b(192);
     if (p.offsets) hipLaunchKernelGGL((sha1_pc4_kernel<false, 2, 16>), g, b, kPc4LdsBytes, stream, p);
     else hipLaunchKernelGGL((sha1_pc4_kernel<true, 2, 16>), g, b, kPc4LdsBytes, stream, p);
+  } else if (variant == 21) {
+    // pc4x2 with its fast loop unrolled by twelve (A/B)
+    static std::once_flag once;
+    std::call_once(once, [] {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4x2_diag_kernel<false, 2, true, 3, false, 12>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, kPc4x2LdsBytes);
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4x2_diag_kernel<true, 2, true, 3, false, 12>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, kPc4x2LdsBytes);
+    });
+    const uint32_t blocks = (p.n + 2 * kPcLanes - 1) / (2 * kPcLanes);
+    if (p.offsets) hipLaunchKernelGGL((sha1_pc4x2_diag_kernel<false, 2, true, 3, false, 12>), dim3(blocks), dim3(384), kPc4x2LdsBytes, stream, p);
+    else hipLaunchKernelGGL((sha1_pc4x2_diag_kernel<true, 2, true, 3, false, 12>), dim3(blocks), dim3(384), kPc4x2LdsBytes, stream, p);
   } else if (variant == 15) {
     // pc4x2 without the six-step loop (diagnostic)
     static std::once_flag once;
     std::call_once(once, [] {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4x2_kernel<false, 2, false>),
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4x2_diag_kernel<false, 2, false, 3, false, 6>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, kPc4x2LdsBytes);
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4x2_kernel<true, 2, false>),
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4x2_diag_kernel<true, 2, false, 3, false, 6>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, kPc4x2LdsBytes);
     });
     const uint32_t blocks = (p.n + 2 * kPcLanes - 1) / (2 * kPcLanes);
-    if (p.offsets) hipLaunchKernelGGL((sha1_pc4x2_kernel<false, 2, false>), dim3(blocks), dim3(384), kPc4x2LdsBytes, stream, p);
-    else hipLaunchKernelGGL((sha1_pc4x2_kernel<true, 2, false>), dim3(blocks), dim3(384), kPc4x2LdsBytes, stream, p);
+    if (p.offsets) hipLaunchKernelGGL((sha1_pc4x2_diag_kernel<false, 2, false, 3, false, 6>), dim3(blocks), dim3(384), kPc4x2LdsBytes, stream, p);
+    else hipLaunchKernelGGL((sha1_pc4x2_diag_kernel<true, 2, false, 3, false, 6>), dim3(blocks), dim3(384), kPc4x2LdsBytes, stream, p);
   } else if (variant == 3) {
     const uint32_t blocks = (p.n + 255) / 256;
     constexpr int lds = 4 * kLdsStages * kPcRawU4 * 16;
@@ -385,7 +397,7 @@ extern "C" int lbf_sha1_uniform_launch(const uint8_t* d_base, uint64_t len, uint
 
 extern "C" int lbf_set_kernel_variant(int variant) {
 #ifdef LBF_EXPERIMENTAL_VARIANTS
-  const bool known = variant >= 0 && variant <= 20;
+  const bool known = variant >= 0 && variant <= 21;
 #else
   const bool known = variant == 0 || variant == 1 || variant == 7 || variant == 10 || variant == 11 || variant == 12;
 #endif
