@@ -198,6 +198,26 @@ def spawn_ranks(n, argv, script=None, python=None, env=None, grace_s=15.0):
     return rc
 
 
+class _stdout_to_stderr:
+    """File descriptor 1 redirected to 2 while in scope (C and C++ writers included)."""
+
+    def __enter__(self):
+        import ctypes
+        self._libc = ctypes.CDLL(None)
+        sys.stdout.flush()
+        self._libc.fflush(None)
+        self._saved = os.dup(1)
+        os.dup2(2, 1)
+        return self
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        self._libc.fflush(None)
+        os.dup2(self._saved, 1)
+        os.close(self._saved)
+        return False
+
+
 def dist_setup(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -214,10 +234,14 @@ def dist_setup(args):
         import torch.distributed as dist
         torch.cuda.set_device(dev)
         backend = os.environ.get("LBF_BENCH_BACKEND", "nccl")
-        if backend == "nccl":
-            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", dev))
-        else:
-            dist.init_process_group(backend, rank=rank, world_size=world)
+        # gloo's C++ side prints its "[Gloo] Rank r is connected to ..." notice on
+        # stdout, where the launcher collects the one JSON line: while the group
+        # forms, the process's stdout points at stderr
+        with _stdout_to_stderr():
+            if backend == "nccl":
+                dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", dev))
+            else:
+                dist.init_process_group(backend, rank=rank, world_size=world)
     else:
         torch.cuda.set_device(0)
     return rank, world, local, dev, ndev

@@ -76,3 +76,33 @@ def test_world_mismatch_under_outside_launcher_is_refused(monkeypatch):
         gpus = 8
     with pytest.raises(SystemExit, match="WORLD_SIZE is 1"):
         bench.dist_setup(A())
+
+
+_GLOO_CHILD = r'''
+import os, sys
+sys.path.insert(0, {root!r})
+import bench
+import torch.distributed as dist
+os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=sys.argv[2])
+with bench._stdout_to_stderr():
+    dist.init_process_group("gloo", rank=int(sys.argv[1]), world_size=2)
+dist.barrier()
+print('{{"rank": %s}}' % sys.argv[1], flush=True)
+dist.destroy_process_group()
+'''
+
+
+def test_gloo_connect_notice_stays_off_stdout(tmp_path):
+    """gloo's C++ side prints "[Gloo] Rank r is connected ..." on stdout while the
+    group forms; under torch.distributed.run that would land next to rank 0's
+    JSON line.  dist_setup forms the group with stdout pointed at stderr."""
+    script = tmp_path / "child.py"
+    script.write_text(_GLOO_CHILD.format(root=ROOT))
+    port = str(bench._free_port())
+    procs = [subprocess.Popen([sys.executable, str(script), str(r), port], stdout=subprocess.PIPE,
+                              stderr=subprocess.PIPE, text=True) for r in range(2)]
+    outs = [p.communicate(timeout=120) for p in procs]
+    assert all(p.returncode == 0 for p in procs), [e[-2000:] for _, e in outs]
+    for r, (out, err) in enumerate(outs):
+        assert out.strip() == '{"rank": %d}' % r, out
+        assert "[Gloo]" in err
