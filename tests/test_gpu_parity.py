@@ -122,6 +122,26 @@ def test_partial_waves_hash_and_verify(variant, hasher, oracle, n):
     assert v[:-1].all() and not v[-1]
 
 
+@pytest.mark.parametrize("long_group", [0, 1])
+def test_groups_of_one_workgroup_with_different_step_counts(variant, hasher, oracle, long_group):
+    """Chains 0..63 and 64..127 share a workgroup in pc4x2 (12) and pcx5 (10):
+    one group's chains a few blocks long, the other's thousands.  Every wave of
+    the workgroup passes the longer group's barriers; the short group's chains
+    must still end at their own last block."""
+    rng = np.random.default_rng(77 + long_group)
+    buf = oracle.synth(37, 0, 8 << 20)
+    n = 256  # two pc4x2 workgroups
+    sizes = rng.integers(0, 300, n).astype(np.uint32)
+    for w in range(0, n, 128):
+        lo = w + 64 * long_group
+        sizes[lo:lo + 64] = rng.integers(200000, 260000, 64)
+    offs = np.array([rng.integers(0, buf.size - s + 1) for s in sizes], dtype=np.uint64)
+    want = oracle.sha1_batch(buf, offs, sizes)
+    assert np.array_equal(hasher.hash_chunks(buf, offs, sizes), want)
+    v = hasher.verify_chunks(buf, offs, sizes, want)
+    assert v.all()
+
+
 def test_empty_inputs(variant, hasher):
     assert hasher.sha1(b"").hex() == "da39a3ee5e6b4b0d3255bfef95601890afd80709"
     out = hasher.hash_chunks(np.zeros(16, np.uint8), np.zeros(0, np.uint64), np.zeros(0, np.uint32))
@@ -230,6 +250,28 @@ def test_device_ptr_batch(variant, hasher, oracle):
     finally:
         for b in (d_data, d_off, d_size, d_out):
             b.free()
+
+
+def test_uniform_ragged_chain_count_between_16k_and_32k(variant, oracle):
+    """20,000 chains -- the automatic choice is pc4x2 there -- with a short last
+    chunk: the last workgroup's second group is partly idle (20,000 = 156 x 128
+    + 32).  Device-resident, every digest against the oracle."""
+    cs = 4096
+    n_bytes = 19999 * cs + 1000
+    n = 20000
+    buf = DeviceBuffer(n_bytes)
+    dig = DeviceBuffer(n * 20)
+    try:
+        buf.fill_synthetic(91)
+        H.uniform_launch(buf, n_bytes, cs, 0, n, dig)
+        H.synchronize()
+        got = dig.download(n * 20).reshape(n, 20)
+        want = oracle.encode_buffer(oracle.synth(91, 0, n_bytes), cs)
+        bad = np.nonzero((got != want).any(axis=1))[0]
+        assert bad.size == 0, f"{bad.size} mismatches, first at {bad[:5]}"
+    finally:
+        buf.free()
+        dig.free()
 
 
 def test_uniform_partial_last_chunk(variant, oracle):
