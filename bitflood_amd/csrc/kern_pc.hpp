@@ -583,6 +583,8 @@ __global__ void __launch_bounds__(192) sha1_pc4_kernel(ChunkParams p) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA outlives the workgroup
   } else {
     // ---------------- consumer ----------------
+    // (No s_setprio here: the consumer is wave 0, the oldest, and priority 3
+    // measured 0.3-0.6 % slower; profiles/r03/pc4x2/prio/.)
     Digest s;
     s.init();
     Pc4Sched<kVec> A, B;
@@ -658,6 +660,10 @@ __global__ void __launch_bounds__(192) sha1_pc4_kernel(ChunkParams p) {
 // barrier s-3 (step 0 is loaded before an extra barrier that ends the
 // prologue).  Both groups pass the same barriers, so every wave counts the
 // steps of both groups' chains.  LDS 152 KiB: one workgroup per CU.
+// The consumers raise their wave priority (s_setprio 3): they are younger than
+// the producers of waves 0 and 1, and the CU's arbiter serves older waves
+// first -- with the priority C4 went from 13.76-13.80 to 13.10-13.11 ms
+// (experimental variant 22 against 12, profiles/r03/pc4x2/prio/).
 // ---------------------------------------------------------------------------
 constexpr int kPc4x2Ring = 3;
 constexpr int kPc4x2GroupU4 = kPc4x2Ring * kPcSlotU4 + 2 * kP2Raw * kPcRawU4;
@@ -695,7 +701,9 @@ __device__ __forceinline__ void pc4x2_store_half(uint32_t (&w)[16], uint4* ring,
 // kFence (experimental variants 18, 19, diagnostics): scheduling barriers
 // around the producers' workgroup barrier, as the stamped build has them.
 // kUnroll6 (a multiple of 6): steps per fast-loop iteration (12: experimental variant 21).
-template <bool kUniform, int kGroups, bool kFast, int kRawAt, bool kFence, int kUnroll6>
+// kPrio (experimental variants 22, 23, diagnostics): the consumers raise their
+// wave priority (s_setprio 3) so the CU's arbiter serves them before producers.
+template <bool kUniform, int kGroups, bool kFast, int kRawAt, bool kFence, int kUnroll6, bool kPrio = false>
 __device__ __forceinline__ void pc4x2_body(const ChunkParams& p) {
   static_assert(kUnroll6 % 6 == 0, "the fast loop keeps k % 6 == 0");
   extern __shared__ __attribute__((aligned(16))) uint4 lds[];  // group 0 | group 1: W[3][20][64] | raw[2][2][4][64]
@@ -763,6 +771,7 @@ __device__ __forceinline__ void pc4x2_body(const ChunkParams& p) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA outlives the workgroup
   } else {
     // ---------------- consumer of group g ----------------
+    if (kPrio) __builtin_amdgcn_s_setprio(3);
     Digest s;
     s.init();
     Pc4Sched<2> A, B;
@@ -816,14 +825,14 @@ __device__ __forceinline__ void pc4x2_body(const ChunkParams& p) {
 // The shipped kernel (variant 12).
 template <bool kUniform>
 __global__ void __launch_bounds__(384) sha1_pc4x2_kernel(ChunkParams p) {
-  pc4x2_body<kUniform, 2, true, kPc4x2Ring, false, 6>(p);
+  pc4x2_body<kUniform, 2, true, kPc4x2Ring, false, 6, true>(p);
 }
 
 #ifdef LBF_EXPERIMENTAL_VARIANTS
 // Diagnostic forms (experimental variants 13-15, 17-19, 21).
-template <bool kUniform, int kGroups, bool kFast, int kRawAt, bool kFence, int kUnroll6>
+template <bool kUniform, int kGroups, bool kFast, int kRawAt, bool kFence, int kUnroll6, bool kPrio = false>
 __global__ void __launch_bounds__(192 * kGroups) sha1_pc4x2_diag_kernel(ChunkParams p) {
-  pc4x2_body<kUniform, kGroups, kFast, kRawAt, kFence, kUnroll6>(p);
+  pc4x2_body<kUniform, kGroups, kFast, kRawAt, kFence, kUnroll6, kPrio>(p);
 }
 #endif
 

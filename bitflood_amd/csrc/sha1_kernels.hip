@@ -286,6 +286,29 @@ bool launch_experimental(int variant, const ChunkParams& p, hipStream_t stream) 
     const uint32_t blocks = (p.n + 2 * kPcLanes - 1) / (2 * kPcLanes);
     if (p.offsets) hipLaunchKernelGGL((sha1_pc4x2_diag_kernel<false, 2, true, 3, false, 12>), dim3(blocks), dim3(384), kPc4x2LdsBytes, stream, p);
     else hipLaunchKernelGGL((sha1_pc4x2_diag_kernel<true, 2, true, 3, false, 12>), dim3(blocks), dim3(384), kPc4x2LdsBytes, stream, p);
+  } else if (variant == 22 || variant == 23) {
+    // pc4x2 (22) and its one-group form (23) with the consumers at wave priority 3 (diagnostics)
+    constexpr int lds1 = 100 * 1024;
+    static std::once_flag once;
+    std::call_once(once, [] {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4x2_diag_kernel<false, 2, true, 3, false, 6, true>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, kPc4x2LdsBytes);
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4x2_diag_kernel<true, 2, true, 3, false, 6, true>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, kPc4x2LdsBytes);
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4x2_diag_kernel<false, 1, true, 3, false, 6, true>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, lds1);
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4x2_diag_kernel<true, 1, true, 3, false, 6, true>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, lds1);
+    });
+    if (variant == 22) {
+      const uint32_t blocks = (p.n + 2 * kPcLanes - 1) / (2 * kPcLanes);
+      if (p.offsets) hipLaunchKernelGGL((sha1_pc4x2_diag_kernel<false, 2, true, 3, false, 6, true>), dim3(blocks), dim3(384), kPc4x2LdsBytes, stream, p);
+      else hipLaunchKernelGGL((sha1_pc4x2_diag_kernel<true, 2, true, 3, false, 6, true>), dim3(blocks), dim3(384), kPc4x2LdsBytes, stream, p);
+    } else {
+      const uint32_t blocks = (p.n + kPcLanes - 1) / kPcLanes;
+      if (p.offsets) hipLaunchKernelGGL((sha1_pc4x2_diag_kernel<false, 1, true, 3, false, 6, true>), dim3(blocks), dim3(192), lds1, stream, p);
+      else hipLaunchKernelGGL((sha1_pc4x2_diag_kernel<true, 1, true, 3, false, 6, true>), dim3(blocks), dim3(192), lds1, stream, p);
+    }
   } else if (variant == 15) {
     // pc4x2 without the six-step loop (diagnostic)
     static std::once_flag once;
@@ -397,7 +420,7 @@ extern "C" int lbf_sha1_uniform_launch(const uint8_t* d_base, uint64_t len, uint
 
 extern "C" int lbf_set_kernel_variant(int variant) {
 #ifdef LBF_EXPERIMENTAL_VARIANTS
-  const bool known = variant >= 0 && variant <= 21;
+  const bool known = variant >= 0 && variant <= 23;
 #else
   const bool known = variant == 0 || variant == 1 || variant == 7 || variant == 10 || variant == 11 || variant == 12;
 #endif
