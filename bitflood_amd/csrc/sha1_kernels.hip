@@ -309,6 +309,18 @@ bool launch_experimental(int variant, const ChunkParams& p, hipStream_t stream) 
       if (p.offsets) hipLaunchKernelGGL((sha1_pc4x2_diag_kernel<false, 1, true, 3, false, 6, true>), dim3(blocks), dim3(192), lds1, stream, p);
       else hipLaunchKernelGGL((sha1_pc4x2_diag_kernel<true, 1, true, 3, false, 6, true>), dim3(blocks), dim3(192), lds1, stream, p);
     }
+  } else if (variant == 25) {
+    // pc4x2 (consumers at priority 3) with group 1's producers at priority 1 (diagnostic)
+    static std::once_flag once;
+    std::call_once(once, [] {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4x2_diag_kernel<false, 2, true, 3, false, 6, true, true>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, kPc4x2LdsBytes);
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4x2_diag_kernel<true, 2, true, 3, false, 6, true, true>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, kPc4x2LdsBytes);
+    });
+    const uint32_t blocks = (p.n + 2 * kPcLanes - 1) / (2 * kPcLanes);
+    if (p.offsets) hipLaunchKernelGGL((sha1_pc4x2_diag_kernel<false, 2, true, 3, false, 6, true, true>), dim3(blocks), dim3(384), kPc4x2LdsBytes, stream, p);
+    else hipLaunchKernelGGL((sha1_pc4x2_diag_kernel<true, 2, true, 3, false, 6, true, true>), dim3(blocks), dim3(384), kPc4x2LdsBytes, stream, p);
   } else if (variant == 15) {
     // pc4x2 without the six-step loop (diagnostic)
     static std::once_flag once;
@@ -420,7 +432,7 @@ extern "C" int lbf_sha1_uniform_launch(const uint8_t* d_base, uint64_t len, uint
 
 extern "C" int lbf_set_kernel_variant(int variant) {
 #ifdef LBF_EXPERIMENTAL_VARIANTS
-  const bool known = variant >= 0 && variant <= 23;
+  const bool known = variant >= 0 && variant <= 25;
 #else
   const bool known = variant == 0 || variant == 1 || variant == 7 || variant == 10 || variant == 11 || variant == 12;
 #endif
