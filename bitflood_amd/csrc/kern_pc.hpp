@@ -663,7 +663,11 @@ __global__ void __launch_bounds__(192) sha1_pc4_kernel(ChunkParams p) {
 // The consumers raise their wave priority (s_setprio 3): they are younger than
 // the producers of waves 0 and 1, and the CU's arbiter serves older waves
 // first -- with the priority C4 went from 13.76-13.80 to 13.10-13.11 ms
-// (experimental variant 22 against 12, profiles/r03/pc4x2/prio/).
+// (experimental variant 22 against 12, profiles/r03/pc4x2/prio/).  Group 1's
+// producers (waves 4 and 5, the younger of each producer pair on a SIMD) then
+// run at priority 1, which breaks the age order between the two producers of
+// a SIMD: 13.07 -> 12.92 ms at C4, 1.1-1.5 % at every size (experimental
+// variant 25 against 12, profiles/r03/pc4x2/prio/s31_*).
 // ---------------------------------------------------------------------------
 constexpr int kPc4x2Ring = 3;
 constexpr int kPc4x2GroupU4 = kPc4x2Ring * kPcSlotU4 + 2 * kP2Raw * kPcRawU4;
@@ -703,8 +707,8 @@ __device__ __forceinline__ void pc4x2_store_half(uint32_t (&w)[16], uint4* ring,
 // kUnroll6 (a multiple of 6): steps per fast-loop iteration (12: experimental variant 21).
 // kPrio (experimental variants 22, 23, diagnostics): the consumers raise their
 // wave priority (s_setprio 3) so the CU's arbiter serves them before producers.
-// kProdPrio1 (experimental variant 25, a diagnostic): group 1's producers, the
-// younger of each SIMD pair, at wave priority 1.
+// kProdPrio1 (experimental variant 25, then the shipped kernel): group 1's
+// producers, the younger of each SIMD pair, at wave priority 1.
 template <bool kUniform, int kGroups, bool kFast, int kRawAt, bool kFence, int kUnroll6, bool kPrio = false,
           bool kProdPrio1 = false>
 __device__ __forceinline__ void pc4x2_body(const ChunkParams& p) {
@@ -829,7 +833,7 @@ __device__ __forceinline__ void pc4x2_body(const ChunkParams& p) {
 // The shipped kernel (variant 12).
 template <bool kUniform>
 __global__ void __launch_bounds__(384) sha1_pc4x2_kernel(ChunkParams p) {
-  pc4x2_body<kUniform, 2, true, kPc4x2Ring, false, 6, true>(p);
+  pc4x2_body<kUniform, 2, true, kPc4x2Ring, false, 6, true, true>(p);
 }
 
 #ifdef LBF_EXPERIMENTAL_VARIANTS

@@ -310,7 +310,8 @@ bool launch_experimental(int variant, const ChunkParams& p, hipStream_t stream) 
       else hipLaunchKernelGGL((sha1_pc4x2_diag_kernel<true, 1, true, 3, false, 6, true>), dim3(blocks), dim3(192), lds1, stream, p);
     }
   } else if (variant == 25) {
-    // pc4x2 (consumers at priority 3) with group 1's producers at priority 1 (diagnostic)
+    // pc4x2 (consumers at priority 3) with group 1's producers at priority 1: the shipped variant 12's code since
+    // session 32, kept under this number so the A/B of profiles/r03/pc4x2/prio/s31_* can be rerun
     static std::once_flag once;
     std::call_once(once, [] {
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4x2_diag_kernel<false, 2, true, 3, false, 6, true, true>),
