@@ -707,10 +707,10 @@ __device__ __forceinline__ void pc4x2_store_half(uint32_t (&w)[16], uint4* ring,
 // kUnroll6 (a multiple of 6): steps per fast-loop iteration (12: experimental variant 21).
 // kPrio (experimental variants 22, 23, diagnostics): the consumers raise their
 // wave priority (s_setprio 3) so the CU's arbiter serves them before producers.
-// kProdPrio1 (experimental variant 25, then the shipped kernel): group 1's
-// producers, the younger of each SIMD pair, at wave priority 1.
+// kPrioG0, kPrioG1: wave priority of group 0's / group 1's producers (0, 1 in
+// the shipped kernel since experimental variant 25; variants 26-28 try others).
 template <bool kUniform, int kGroups, bool kFast, int kRawAt, bool kFence, int kUnroll6, bool kPrio = false,
-          bool kProdPrio1 = false>
+          int kPrioG0 = 0, int kPrioG1 = 0>
 __device__ __forceinline__ void pc4x2_body(const ChunkParams& p) {
   static_assert(kUnroll6 % 6 == 0, "the fast loop keeps k % 6 == 0");
   extern __shared__ __attribute__((aligned(16))) uint4 lds[];  // group 0 | group 1: W[3][20][64] | raw[2][2][4][64]
@@ -739,7 +739,8 @@ __device__ __forceinline__ void pc4x2_body(const ChunkParams& p) {
 
   if (wave != 2 && wave != 3) {
     // ---------------- producer X of group g: steps X, X+2, ... ----------------
-    if (kProdPrio1 && g == 1) __builtin_amdgcn_s_setprio(1);
+    if (kPrioG0 != 0 && g == 0) __builtin_amdgcn_s_setprio(kPrioG0);
+    if (kPrioG1 != 0 && g == 1) __builtin_amdgcn_s_setprio(kPrioG1);
     const uint32_t X = g == 0 ? wave : wave - 4;
     uint4* raw = ring + kRawAt * kPcSlotU4 + X * (kP2Raw * kPcRawU4);
     const uint32_t raw_lds = (uint32_t)reinterpret_cast<uintptr_t>(raw);
@@ -833,15 +834,15 @@ __device__ __forceinline__ void pc4x2_body(const ChunkParams& p) {
 // The shipped kernel (variant 12).
 template <bool kUniform>
 __global__ void __launch_bounds__(384) sha1_pc4x2_kernel(ChunkParams p) {
-  pc4x2_body<kUniform, 2, true, kPc4x2Ring, false, 6, true, true>(p);
+  pc4x2_body<kUniform, 2, true, kPc4x2Ring, false, 6, true, 0, 1>(p);
 }
 
 #ifdef LBF_EXPERIMENTAL_VARIANTS
 // Diagnostic forms (experimental variants 13-15, 17-19, 21).
 template <bool kUniform, int kGroups, bool kFast, int kRawAt, bool kFence, int kUnroll6, bool kPrio = false,
-          bool kProdPrio1 = false>
+          int kPrioG0 = 0, int kPrioG1 = 0>
 __global__ void __launch_bounds__(192 * kGroups) sha1_pc4x2_diag_kernel(ChunkParams p) {
-  pc4x2_body<kUniform, kGroups, kFast, kRawAt, kFence, kUnroll6, kPrio, kProdPrio1>(p);
+  pc4x2_body<kUniform, kGroups, kFast, kRawAt, kFence, kUnroll6, kPrio, kPrioG0, kPrioG1>(p);
 }
 #endif
 

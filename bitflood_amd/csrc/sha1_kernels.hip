@@ -157,6 +157,21 @@ void launch_lane(const ChunkParams& p, hipStream_t stream) {
 }
 
 #ifdef LBF_EXPERIMENTAL_VARIANTS
+// pc4x2, consumers at priority 3, producers of group 0 / group 1 at kP0 / kP1
+template <int kP0, int kP1>
+void launch_pc4x2_prio(const ChunkParams& p, hipStream_t stream) {
+  static std::once_flag once;
+  std::call_once(once, [] {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4x2_diag_kernel<false, 2, true, 3, false, 6, true, kP0, kP1>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, kPc4x2LdsBytes);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4x2_diag_kernel<true, 2, true, 3, false, 6, true, kP0, kP1>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, kPc4x2LdsBytes);
+  });
+  const uint32_t blocks = (p.n + 2 * kPcLanes - 1) / (2 * kPcLanes);
+  if (p.offsets) hipLaunchKernelGGL((sha1_pc4x2_diag_kernel<false, 2, true, 3, false, 6, true, kP0, kP1>), dim3(blocks), dim3(384), kPc4x2LdsBytes, stream, p);
+  else hipLaunchKernelGGL((sha1_pc4x2_diag_kernel<true, 2, true, 3, false, 6, true, kP0, kP1>), dim3(blocks), dim3(384), kPc4x2LdsBytes, stream, p);
+}
+
 // Superseded variants, kept for A/B sweeps: false when `variant` is not one.
 bool launch_experimental(int variant, const ChunkParams& p, hipStream_t stream) {
   if (variant == 2) {
@@ -309,19 +324,14 @@ bool launch_experimental(int variant, const ChunkParams& p, hipStream_t stream) 
       if (p.offsets) hipLaunchKernelGGL((sha1_pc4x2_diag_kernel<false, 1, true, 3, false, 6, true>), dim3(blocks), dim3(192), lds1, stream, p);
       else hipLaunchKernelGGL((sha1_pc4x2_diag_kernel<true, 1, true, 3, false, 6, true>), dim3(blocks), dim3(192), lds1, stream, p);
     }
-  } else if (variant == 25) {
-    // pc4x2 (consumers at priority 3) with group 1's producers at priority 1: the shipped variant 12's code since
-    // session 32, kept under this number so the A/B of profiles/r03/pc4x2/prio/s31_* can be rerun
-    static std::once_flag once;
-    std::call_once(once, [] {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4x2_diag_kernel<false, 2, true, 3, false, 6, true, true>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, kPc4x2LdsBytes);
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4x2_diag_kernel<true, 2, true, 3, false, 6, true, true>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, kPc4x2LdsBytes);
-    });
-    const uint32_t blocks = (p.n + 2 * kPcLanes - 1) / (2 * kPcLanes);
-    if (p.offsets) hipLaunchKernelGGL((sha1_pc4x2_diag_kernel<false, 2, true, 3, false, 6, true, true>), dim3(blocks), dim3(384), kPc4x2LdsBytes, stream, p);
-    else hipLaunchKernelGGL((sha1_pc4x2_diag_kernel<true, 2, true, 3, false, 6, true, true>), dim3(blocks), dim3(384), kPc4x2LdsBytes, stream, p);
+  } else if (variant >= 25 && variant <= 28) {
+    // pc4x2 (consumers at priority 3) with its producers at wave priorities (group 0, group 1): 25 (0, 1) is the
+    // shipped variant 12's code since session 32, kept so the A/B of profiles/r03/pc4x2/prio/s31_* can be rerun;
+    // 26 (1, 0), 27 (0, 2), 28 (1, 2)
+    if (variant == 25) launch_pc4x2_prio<0, 1>(p, stream);
+    else if (variant == 26) launch_pc4x2_prio<1, 0>(p, stream);
+    else if (variant == 27) launch_pc4x2_prio<0, 2>(p, stream);
+    else launch_pc4x2_prio<1, 2>(p, stream);
   } else if (variant == 15) {
     // pc4x2 without the six-step loop (diagnostic)
     static std::once_flag once;
@@ -433,7 +443,7 @@ extern "C" int lbf_sha1_uniform_launch(const uint8_t* d_base, uint64_t len, uint
 
 extern "C" int lbf_set_kernel_variant(int variant) {
 #ifdef LBF_EXPERIMENTAL_VARIANTS
-  const bool known = variant >= 0 && variant <= 25;
+  const bool known = variant >= 0 && variant <= 28;
 #else
   const bool known = variant == 0 || variant == 1 || variant == 7 || variant == 10 || variant == 11 || variant == 12;
 #endif
