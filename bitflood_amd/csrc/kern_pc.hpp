@@ -528,7 +528,15 @@ __device__ __forceinline__ void pc4_barrier(Digest& s PC4_ACC_ARGS) {
 // kUnroll: steps per fast-loop iteration.  Eight since round 3: 0.3-1.1 %
 // faster than four at C2 in alternating runs (profiles/r03/pc4x2/diag/sweep_7_16_*.jsonl);
 // four is experimental variant 16, for A/B.
+// kPrioP0, kPrioP1: wave priority of producer 0 / producer 1 (waves 1 and 2),
+// template parameters only in the experimental build (variants 29-31); the
+// shipped build has the constants 0 below, so its kernel is unchanged.
+#ifdef LBF_EXPERIMENTAL_VARIANTS
+template <bool kUniform, int kVec, int kUnroll = 8, int kPrioP0 = 0, int kPrioP1 = 0>
+#else
+constexpr int kPrioP0 = 0, kPrioP1 = 0;
 template <bool kUniform, int kVec, int kUnroll = 8>
+#endif
 __global__ void __launch_bounds__(192) sha1_pc4_kernel(ChunkParams p) {
   extern __shared__ __attribute__((aligned(16))) uint4 ring[];  // W[3][20][64] | raw[2][2][4][64]
   const int lane = threadIdx.x & 63;
@@ -546,6 +554,8 @@ __global__ void __launch_bounds__(192) sha1_pc4_kernel(ChunkParams p) {
   if (wave != 0) {
     // ---------------- producer X = wave - 1: steps X, X+2, ... ----------------
     const uint32_t X = wave - 1;
+    if (kPrioP0 != 0 && X == 0) __builtin_amdgcn_s_setprio(kPrioP0);
+    if (kPrioP1 != 0 && X == 1) __builtin_amdgcn_s_setprio(kPrioP1);
     uint4* raw = ring + kPc4Ring * kPcSlotU4 + X * (kP2Raw * kPcRawU4);
     const uint32_t raw_lds = (uint32_t)reinterpret_cast<uintptr_t>(raw);
     p2_dma(c, X, raw_lds, 0);
@@ -599,7 +609,7 @@ __global__ void __launch_bounds__(192) sha1_pc4_kernel(ChunkParams p) {
       __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
     }
     uint32_t k = 0;
-    // Four steps per iteration while every chain of the workgroup is running
+    // kUnroll steps per iteration while every chain of the workgroup is running
     // and every step is followed by a barrier: k % 4 == 0, so the slots are
     // compile-time offsets and the steps need no liveness checks.  The two
     // conditions are folded into one bound, so the loop test is one scalar

@@ -172,6 +172,21 @@ void launch_pc4x2_prio(const ChunkParams& p, hipStream_t stream) {
   else hipLaunchKernelGGL((sha1_pc4x2_diag_kernel<true, 2, true, 3, false, 6, true, kP0, kP1>), dim3(blocks), dim3(384), kPc4x2LdsBytes, stream, p);
 }
 
+// pc4 with its producers (waves 1, 2) at wave priorities kP0 / kP1
+template <int kP0, int kP1>
+void launch_pc4_prio(const ChunkParams& p, hipStream_t stream) {
+  static std::once_flag once;
+  std::call_once(once, [] {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4_kernel<false, 2, 8, kP0, kP1>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, kPc4LdsBytes);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4_kernel<true, 2, 8, kP0, kP1>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, kPc4LdsBytes);
+  });
+  const dim3 g((p.n + kPcLanes - 1) / kPcLanes), b(192);
+  if (p.offsets) hipLaunchKernelGGL((sha1_pc4_kernel<false, 2, 8, kP0, kP1>), g, b, kPc4LdsBytes, stream, p);
+  else hipLaunchKernelGGL((sha1_pc4_kernel<true, 2, 8, kP0, kP1>), g, b, kPc4LdsBytes, stream, p);
+}
+
 // Superseded variants, kept for A/B sweeps: false when `variant` is not one.
 bool launch_experimental(int variant, const ChunkParams& p, hipStream_t stream) {
   if (variant == 2) {
@@ -324,6 +339,11 @@ bool launch_experimental(int variant, const ChunkParams& p, hipStream_t stream) 
       if (p.offsets) hipLaunchKernelGGL((sha1_pc4x2_diag_kernel<false, 1, true, 3, false, 6, true>), dim3(blocks), dim3(192), lds1, stream, p);
       else hipLaunchKernelGGL((sha1_pc4x2_diag_kernel<true, 1, true, 3, false, 6, true>), dim3(blocks), dim3(192), lds1, stream, p);
     }
+  } else if (variant >= 29 && variant <= 31) {
+    // pc4 with producer priorities (producer 0, producer 1): 29 (0, 1), 30 (1, 0), 31 (1, 1)
+    if (variant == 29) launch_pc4_prio<0, 1>(p, stream);
+    else if (variant == 30) launch_pc4_prio<1, 0>(p, stream);
+    else launch_pc4_prio<1, 1>(p, stream);
   } else if (variant >= 25 && variant <= 28) {
     // pc4x2 (consumers at priority 3) with its producers at wave priorities (group 0, group 1): 25 (0, 1) is the
     // shipped variant 12's code since session 32, kept so the A/B of profiles/r03/pc4x2/prio/s31_* can be rerun;
@@ -443,7 +463,7 @@ extern "C" int lbf_sha1_uniform_launch(const uint8_t* d_base, uint64_t len, uint
 
 extern "C" int lbf_set_kernel_variant(int variant) {
 #ifdef LBF_EXPERIMENTAL_VARIANTS
-  const bool known = variant >= 0 && variant <= 28;
+  const bool known = variant >= 0 && variant <= 31;
 #else
   const bool known = variant == 0 || variant == 1 || variant == 7 || variant == 10 || variant == 11 || variant == 12;
 #endif
