@@ -529,7 +529,7 @@ __device__ __forceinline__ void pc4_barrier(Digest& s PC4_ACC_ARGS) {
 // faster than four at C2 in alternating runs (profiles/r03/pc4x2/diag/sweep_7_16_*.jsonl);
 // four is experimental variant 16, for A/B.
 // kPrioP0, kPrioP1: wave priority of producer 0 / producer 1 (waves 1 and 2),
-// template parameters only in the experimental build (variants 29-31); the
+// template parameters only in the experimental build (variants 29-33); the
 // shipped build has the constants 0 below, so its kernel is unchanged.
 #ifdef LBF_EXPERIMENTAL_VARIANTS
 template <bool kUniform, int kVec, int kUnroll = 8, int kPrioP0 = 0, int kPrioP1 = 0>

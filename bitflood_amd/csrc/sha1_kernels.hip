@@ -339,11 +339,13 @@ bool launch_experimental(int variant, const ChunkParams& p, hipStream_t stream) 
       if (p.offsets) hipLaunchKernelGGL((sha1_pc4x2_diag_kernel<false, 1, true, 3, false, 6, true>), dim3(blocks), dim3(192), lds1, stream, p);
       else hipLaunchKernelGGL((sha1_pc4x2_diag_kernel<true, 1, true, 3, false, 6, true>), dim3(blocks), dim3(192), lds1, stream, p);
     }
-  } else if (variant >= 29 && variant <= 31) {
-    // pc4 with producer priorities (producer 0, producer 1): 29 (0, 1), 30 (1, 0), 31 (1, 1)
+  } else if (variant >= 29 && variant <= 33) {
+    // pc4 with producer priorities (producer 0, producer 1): 29 (0, 1), 30 (1, 0), 31 (1, 1), 32 (2, 2), 33 (3, 3)
     if (variant == 29) launch_pc4_prio<0, 1>(p, stream);
     else if (variant == 30) launch_pc4_prio<1, 0>(p, stream);
-    else launch_pc4_prio<1, 1>(p, stream);
+    else if (variant == 31) launch_pc4_prio<1, 1>(p, stream);
+    else if (variant == 32) launch_pc4_prio<2, 2>(p, stream);
+    else launch_pc4_prio<3, 3>(p, stream);
   } else if (variant >= 25 && variant <= 28) {
     // pc4x2 (consumers at priority 3) with its producers at wave priorities (group 0, group 1): 25 (0, 1) is the
     // shipped variant 12's code since session 32, kept so the A/B of profiles/r03/pc4x2/prio/s31_* can be rerun;
@@ -463,7 +465,7 @@ extern "C" int lbf_sha1_uniform_launch(const uint8_t* d_base, uint64_t len, uint
 
 extern "C" int lbf_set_kernel_variant(int variant) {
 #ifdef LBF_EXPERIMENTAL_VARIANTS
-  const bool known = variant >= 0 && variant <= 31;
+  const bool known = variant >= 0 && variant <= 33;
 #else
   const bool known = variant == 0 || variant == 1 || variant == 7 || variant == 10 || variant == 11 || variant == 12;
 #endif
