@@ -22,8 +22,8 @@ except Exception:  # pragma: no cover - torch is part of the image
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _REPO = os.path.dirname(_HERE)
 # LBF_LIB: tools only (tools/sweep_variants.py, tools/fuzz_gpu.py) point it at
-# the experimental build (`make -C bitflood_amd/csrc experimental`) that also
-# carries the superseded kernel variants; the product loads the shipped one.
+# the A/B library of tools/experimental/ (`make -C tools/experimental`) that
+# also carries the superseded kernel variants; the product loads the shipped one.
 LIB_PATH = os.environ.get("LBF_LIB") or os.path.join(_HERE, "lib", "liblbfhash.so")
 HEADER_PATH = os.path.join(_REPO, "include", "lbf_hash.h")
 

@@ -1,6 +1,6 @@
 // kern_lane.hpp -- one chunk per lane: "lane" (variant 1) and "lds2" (11),
-// the kernels for many chains (every SIMD busy); "lds" (3) only in the
-// LBF_EXPERIMENTAL_VARIANTS build.
+// the kernels for many chains (every SIMD busy).  "lds2" grew out of "lds"
+// (variant 3: one 64-byte block per DMA step), kept in tools/experimental/.
 //
 // Part of the single translation unit sha1_kernels.hip (included from there);
 // DESIGN.md §4 has the measurements behind each kernel.
@@ -93,85 +93,16 @@ __global__ void __launch_bounds__(256) sha1_lane_kernel(ChunkParams p) {
 }
 
 
-#ifdef LBF_EXPERIMENTAL_VARIANTS  // not shipped: superseded by lds2 (variant 11)
 // ---------------------------------------------------------------------------
-// Kernel "lds" (variant 3): one chunk per lane for MANY chains.
+// Kernel "lds2" (variant 11): one chunk per lane for MANY chains, fetching
+// each chain's bytes a whole 128-B line at a time.
 //
 // With >= 4 waves per SIMD the VALU itself is the limit (≈2,040 SIMD cycles per
 // 64-byte block) and what is left to win is memory stall: in the
 // lane kernel the compiler sinks every 16-byte load next to its use, so each
-// block waits a full HBM round trip.  Here each wave streams its 64 chains'
-// next kStages blocks global -> LDS with DMA (no VGPRs in flight, so the
-// compiler cannot move them) and waits by count.  LDS per wave: kStages x 4 KiB.
-// ---------------------------------------------------------------------------
-template <int kStages>
-__device__ __forceinline__ void lds_dma_step(const ChainInfo& c, uint32_t step, uint32_t wave_lds) {
-  const bool ok = c.aligned && step < c.nfull;
-  const uint8_t* src = ok ? c.src + 64ull * step : reinterpret_cast<const uint8_t*>(g_pc_dummy);
-  const uint32_t slot = wave_lds + (step % kStages) * (kPcRawU4 * 16);
-#pragma unroll
-  for (int j = 0; j < 4; ++j) dma16(src + 16 * j, slot + j * (kPcLanes * 16));
-}
-
-template <bool kUniform, int kStages>
-__global__ void __launch_bounds__(256) sha1_lds_kernel(ChunkParams p) {
-  extern __shared__ __attribute__((aligned(16))) uint4 stage[];  // [wave][kStages][4][64]
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  const ChainInfo c = chain_info<kUniform>(p, i);
-  uint4* mine = stage + wave * (kStages * kPcRawU4);
-  const uint32_t wave_lds = (uint32_t)reinterpret_cast<uintptr_t>(mine);
-  const uint32_t nsteps = __builtin_amdgcn_readfirstlane(wave_max(c.nfull));
-  const bool any_unaligned = __builtin_amdgcn_readfirstlane(
-      (uint32_t)(__ballot(c.total != 0 && !c.aligned) != 0));
-  Digest s;
-  s.init();
-#pragma unroll
-  for (uint32_t k = 0; k < (uint32_t)kStages; ++k) lds_dma_step<kStages>(c, k, wave_lds);
-  for (uint32_t k = 0; k < nsteps; ++k) {
-    // block k has landed once at most the (kStages-1) younger steps are pending
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (kStages - 1)) : "memory");
-    const uint4* raw = mine + (k % kStages) * kPcRawU4 + lane;
-    uint32_t w[16];
-    block_from_vec(w, raw[0], raw[kPcLanes], raw[2 * kPcLanes], raw[3 * kPcLanes]);
-    if (any_unaligned && !c.aligned && k < c.nfull) {
-      load_words_any(w, c.src + 64ull * k, 64);
-#pragma unroll
-      for (int q = 0; q < 16; ++q) w[q] = bswap(w[q]);
-    }
-    // the slot is refilled below: its ds_reads must have returned first
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    lds_dma_step<kStages>(c, k + kStages, wave_lds);
-    if (k < c.nfull) compress(s, w);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA outlives the wave
-  if (i >= p.n) return;
-  finish(s, c.src + 64ull * c.nfull, c.size & 63u, c.size);
-  uint32_t be[5];
-#pragma unroll
-  for (int k = 0; k < 5; ++k) be[k] = bswap(s.h[k]);
-  if (p.digests) {
-    uint32_t* o = reinterpret_cast<uint32_t*>(p.digests + 20ull * i);
-#pragma unroll
-    for (int k = 0; k < 5; ++k) o[k] = be[k];
-  }
-  if (p.verdicts) {
-    const uint32_t* e = reinterpret_cast<const uint32_t*>(p.expected + 20ull * i);
-    uint32_t diff = 0;
-#pragma unroll
-    for (int k = 0; k < 5; ++k) diff |= be[k] ^ e[k];
-    p.verdicts[i] = diff == 0 ? 1 : 0;
-  }
-}
-constexpr int kLdsStages = 2;
-#endif  // LBF_EXPERIMENTAL_VARIANTS
-
-// ---------------------------------------------------------------------------
-// Kernel "lds2" (variant 11): `lds` fetching each chain's bytes a whole 128-B
-// line at a time.
-//
-// `lds` DMAs one 64-byte block per lane per step, so the two halves of a 128-B
+// block waits a full HBM round trip.  Each wave streams its 64 chains' next
+// blocks global -> LDS with DMA (no VGPRs in flight, so the compiler cannot
+// move them) and waits by count.  The first form, `lds`, DMAs one 64-byte block per lane per step, so the two halves of a 128-B
 // line are requested one step (≈2 M other lines chip-wide at C3) apart and
 // HBM traffic reads 1.14 x algorithmic at 262 K chains (profiles/r01/c3_lds).
 // Here the DMA for blocks 2j and 2j+1 goes out as 8 back-to-back instructions,

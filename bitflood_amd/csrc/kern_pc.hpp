@@ -1,8 +1,8 @@
-// kern_pc.hpp -- producer/consumer kernels with one 64-chain pair per
-// workgroup, the kernels for few chains (C2): "pc4" reading its schedule as
-// 8-byte pairs (variant 7) is shipped; "pc" (2, and pcx2 = two pairs, 5),
-// "pc2" (4) and the other pc4 layouts (6, 8) are built only with
-// LBF_EXPERIMENTAL_VARIANTS (make experimental), for A/B sweeps.
+// kern_pc.hpp -- producer/consumer kernels for few chains: "pc4" (variant 7,
+// one 64-chain group per workgroup, C2) and "pc4x2" (variant 12, two groups per
+// workgroup, 16 K-32 K chains, C4 per GPU).  The superseded forms they grew out
+// of (pc, pcx2, pc2, pc4 with uint4 or single loads, the pc4x2 diagnostics)
+// live in tools/experimental/, outside the shipped library.
 //
 // Part of the single translation unit sha1_kernels.hip (included from there);
 // DESIGN.md §4 has the measurements behind each kernel.
@@ -15,178 +15,10 @@
 namespace lbf {
 namespace {
 
-#ifdef LBF_EXPERIMENTAL_VARIANTS  // not shipped: pc (2) and pcx2 (5), superseded by pc4 / pcx5
-// ---------------------------------------------------------------------------
-// Kernel "pc" (variant 2): producer/consumer split for few chains.
-//
-// With few chunks (C2: 16,384 chains = 256 waves for 1,024 SIMDs) a lone wave
-// issues at most one VALU every ~4 cycles (tools/probe_issue.hip), so the time
-// per chunk is set by the instruction count of ONE chain.  The 64-word message
-// expansion and the byte swaps do not depend on the chain state, so a producer
-// wave on another SIMD computes them and hands the 80 expanded words per block
-// over in LDS; the consumer wave runs only the 80 rounds (5 VALU each).
-//
-// One workgroup = 64 chains = 2 waves: wave 0 consumes, wave 1 produces.  The
-// LDS ring has 2 slots of [20 uint4][64 lanes] (20 KiB each); one workgroup
-// barrier per block step separates "producer writes slot k+1" from "consumer
-// reads slot k".  The producer keeps kPcPrefetch blocks of raw chunk bytes in
-// flight in registers.  Final (padding/length) blocks are built by the
-// producer as ordinary steps, so the consumer loop is uniform.
-// ---------------------------------------------------------------------------
-// Raw bytes of block `step` of every chain into raw slot step % 4, laid out
-// [16-byte piece j][lane] so both the DMA and the later ds_read_b128 are
-// contiguous across lanes.  Always exactly 4 VMEM instructions.
-__device__ __forceinline__ void pc_dma_step(const ChainInfo& c, uint32_t step, uint32_t raw_lds) {
-  const bool ok = c.aligned && step < c.nfull;
-  const uint8_t* src = ok ? c.src + 64ull * step : reinterpret_cast<const uint8_t*>(g_pc_dummy);
-  const uint32_t slot = raw_lds + (step % kPcRawSlots) * (kPcRawU4 * 16);
-#pragma unroll
-  for (int j = 0; j < 4; ++j) dma16(src + 16 * j, slot + j * (kPcLanes * 16));
-}
-
-template <int kRing>
-__device__ __forceinline__ void pc_produce(uint4* ring, const ChainInfo& c, uint32_t step, int lane) {
-  uint32_t w[16];
-  if (step < c.nfull) {
-    if (c.aligned) {
-      const uint4* raw = ring + kRing * kPcSlotU4 + (step % kPcRawSlots) * kPcRawU4 + lane;
-      block_from_vec(w, raw[0], raw[kPcLanes], raw[2 * kPcLanes], raw[3 * kPcLanes]);
-    } else {
-      load_words_any(w, c.src + 64ull * step, 64);
-#pragma unroll
-      for (int k = 0; k < 16; ++k) w[k] = bswap(w[k]);
-    }
-  } else {
-    // step == nfull: block with the tail bytes; step == nfull + 1: zeros + length.
-    // Steps past `total` produce don't-care words the consumer never reads.
-    final_block(w, c.src + 64ull * c.nfull, c.size & 63u, c.size, step != c.nfull);
-  }
-  expand_store(w, ring + (step % kRing) * kPcSlotU4 + lane, kPcLanes);
-}
-
-// kRing = 2 (the shipped form): the producer writes step k+1 into slot
-// (k+1) % 2 while the consumer computes step k from slot k % 2.  A 3-slot ring
-// that let the consumer prefetch step k+1 across the barrier measured 6 % slower
-// (extra VGPR traffic and LDS instructions inside the round chain).
-// kPairs consumer/producer pairs per workgroup (waves 0..kPairs-1 consume,
-// kPairs..2*kPairs-1 produce; pair q = wave % kPairs).  kPairs = 2 with 112 KiB
-// of LDS pins ONE workgroup per CU, so each of its 4 waves has a SIMD to itself
-// -- for 16 K-32 K chains, where two 2- or 3-wave workgroups per CU would put
-// a consumer and a producer on one SIMD.
-template <bool kUniform, int kRing, int kPairs = 1>
-__global__ void __launch_bounds__(128 * kPairs) sha1_pc_kernel(ChunkParams p) {
-  extern __shared__ __attribute__((aligned(16))) uint4 lds_all[];  // per pair: W[kRing][20][64] | raw[4][4][64]
-  const int lane = threadIdx.x & 63;
-  const int wave_id = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int pair = wave_id % kPairs;
-  const int wave = wave_id / kPairs;  // 0 = consumer, 1 = producer
-  uint4* ring = lds_all + pair * (pc_lds_bytes<kRing>() / 16);
-  const uint32_t i = blockIdx.x * (kPcLanes * kPairs) + pair * kPcLanes + lane;
-  const ChainInfo c = chain_info<kUniform>(p, i);
-  // Identical in every wave of the workgroup (every wave passes every
-  // barrier); readfirstlane keeps the loop bounds scalar.
-  uint32_t nsteps = __builtin_amdgcn_readfirstlane(wave_max(c.total));
-  if (kPairs > 1) {
-    __shared__ uint32_t wg_steps;
-    if (threadIdx.x == 0) wg_steps = 0;
-    __syncthreads();
-    if (lane == 0) atomicMax(&wg_steps, nsteps);
-    __syncthreads();
-    nsteps = __builtin_amdgcn_readfirstlane(wg_steps);
-  }
-  const uint32_t nbarriers = nsteps;  // both waves pass exactly nsteps barriers
-  constexpr uint32_t kAhead = kRing - 1;  // steps the producer runs ahead
-#ifdef LBF_PC_STAMPS
-  unsigned long long acc[4] = {0, 0, 0, 0}, t0 = 0, t1 = 0, t2 = 0, t3 = 0;
-#endif
-
-  if (wave == 1) {
-    // ---------------- producer ----------------
-    const uint32_t raw_lds = (uint32_t)reinterpret_cast<uintptr_t>(ring + kRing * kPcSlotU4);
-#pragma unroll
-    for (uint32_t s = 0; s < kPcRawSlots; ++s) pc_dma_step(c, s, raw_lds);
-    // steps 0 .. kAhead-1 before the first barrier, then step k + kAhead in interval k
-    for (uint32_t k = 0; k < nbarriers + kAhead - 1; ++k) {
-      if (k < nsteps) {
-        PC_STAMP(t0);
-        // raw block k has landed once at most the 3 younger steps (12 DMAs) are pending
-        asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-        PC_STAMP(t1);
-        pc_produce<kRing>(ring, c, k, lane);
-        pc_dma_step(c, k + kPcRawSlots, raw_lds);  // reuses slot k % 4 (read above)
-        PC_STAMP(t2);
-        PC_ACC(0, t0, t1);
-        PC_ACC(1, t1, t2);
-      }
-      PC_STAMP(t2);
-      if (k + 1 >= kAhead) __syncthreads();       // barrier (k + 1 - kAhead)
-      PC_STAMP(t3);
-      PC_ACC(2, t2, t3);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA outlives the workgroup
-  } else {
-    // ---------------- consumer ----------------
-    Digest s;
-    s.init();
-    const RoundK K;
-    for (uint32_t k = 0; k < nsteps; ++k) {
-      PC_STAMP(t0);
-      __syncthreads();  // barrier k: slot k % 2 complete
-      PC_STAMP(t1);
-      if (k < c.total) compress_expanded(s, ring + (k % kRing) * kPcSlotU4 + lane, kPcLanes, K);
-      PC_STAMP(t2);
-      PC_ACC(0, t0, t1);
-      PC_ACC(1, t1, t2);
-    }
-    if (i < p.n) {
-      uint32_t be[5];
-#pragma unroll
-      for (int k = 0; k < 5; ++k) be[k] = bswap(s.h[k]);
-      if (p.digests) {
-        uint32_t* o = reinterpret_cast<uint32_t*>(p.digests + 20ull * i);
-#pragma unroll
-        for (int k = 0; k < 5; ++k) o[k] = be[k];
-      }
-      if (p.verdicts) {
-        const uint32_t* e = reinterpret_cast<const uint32_t*>(p.expected + 20ull * i);
-        uint32_t diff = 0;
-#pragma unroll
-        for (int k = 0; k < 5; ++k) diff |= be[k] ^ e[k];
-        p.verdicts[i] = diff == 0 ? 1 : 0;
-      }
-    }
-  }
-#ifdef LBF_PC_STAMPS
-  if (lane == 0) {
-    unsigned long long* o = g_pc_stamps + (blockIdx.x * 2 * kPairs + wave_id) * 4;
-    o[0] = acc[0];
-    o[1] = acc[1];
-    o[2] = acc[2];
-    o[3] = nsteps;
-  }
-#endif
-}
-
-#endif  // LBF_EXPERIMENTAL_VARIANTS
-
-// ---------------------------------------------------------------------------
-// Kernel "pc2" (variant 4): one consumer, TWO producers per 64 chains.
-//
-// The consumer's round is cheapest (five VALU ops issued back to back) when
-// its schedule word already carries the round constant, leaving one v_add_u32
-// and one v_add3_u32 for the sum.  Adding K costs the producer 80 more ops per
-// block, more than one producer wave has to spare, so two producers alternate
-// blocks: producer X builds steps X, X+2, X+4, ... and spends two barrier
-// intervals on each (words 0..39 before the first, 40..79 before the second).
-// W ring: 3 slots (step k in slot k % 3): a slot is rewritten only after the
-// consumer has passed the barrier that ends its read.  Raw staging: 2 slots of
-// 4 KiB per producer.  LDS 76 KiB -> two workgroups per CU.
-// ---------------------------------------------------------------------------
-constexpr int kP2Raw = 2;  // raw slots per producer (pc2 and pc4)
-#ifdef LBF_EXPERIMENTAL_VARIANTS
-constexpr int kP2Ring = 3;
-constexpr int kP2LdsBytes = (kP2Ring * kPcSlotU4 + 2 * kP2Raw * kPcRawU4) * 16;
-#endif
+// Producer side shared by pc4 and pc4x2: two producer waves per 64 chains
+// alternate block steps (producer X builds steps X, X+2, ...), each staging its
+// chains' raw blocks in two 4 KiB LDS slots filled by LDS-DMA.
+constexpr int kP2Raw = 2;  // raw slots per producer
 
 // Raw bytes of `step` into raw slot `slot` of this producer: 4 DMA ops always.
 __device__ __forceinline__ void p2_dma(const ChainInfo& c, uint32_t step, uint32_t raw_lds, uint32_t slot) {
@@ -219,102 +51,15 @@ __device__ __forceinline__ void p2_block(uint32_t (&w)[16], const uint4* raw, co
   }
 }
 
-#ifdef LBF_EXPERIMENTAL_VARIANTS  // not shipped: pc2 (4), superseded by pc4
-template <bool kUniform>
-__global__ void __launch_bounds__(192) sha1_pc2_kernel(ChunkParams p) {
-  extern __shared__ __attribute__((aligned(16))) uint4 ring[];  // W[3][20][64] | raw[2][2][4][64]
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t i = blockIdx.x * kPcLanes + lane;
-  const ChainInfo c = chain_info<kUniform>(p, i);
-  const uint32_t nsteps = __builtin_amdgcn_readfirstlane(wave_max(c.total));
-#ifdef LBF_PC_STAMPS
-  unsigned long long acc[4] = {0, 0, 0, 0}, t0 = 0, t1 = 0, t2 = 0, t3 = 0;
-#endif
-
-  if (wave != 0) {
-    // ---------------- producer X = wave - 1: steps X, X+2, ... ----------------
-    const uint32_t X = wave - 1;
-    uint4* raw = ring + kP2Ring * kPcSlotU4 + X * (kP2Raw * kPcRawU4);
-    const uint32_t raw_lds = (uint32_t)reinterpret_cast<uintptr_t>(raw);
-    p2_dma(c, X, raw_lds, 0);
-    p2_dma(c, X + 2, raw_lds, 1);
-    uint32_t w[16];
-    // Interval b ends at barrier b.  Producer X finishes step b when b % 2 == X
-    // and starts step b + 1 otherwise; producer 0 builds step 0 whole.
-    for (uint32_t b = 0; b < nsteps; ++b) {
-      const bool second = (b & 1u) == X;
-      const uint32_t step = second ? b : b + 1;
-      const bool first_too = (b == 0 && X == 0);
-      PC_STAMP(t0);
-      PC_COPY(t1, t0);
-      if ((!second || first_too) && step < nsteps) {
-        const uint32_t j = (step - X) >> 1;  // this producer's j-th step
-        // block j has landed once only block j+1's 4 DMAs may be pending
-        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        PC_STAMP(t1);
-        p2_block(w, raw + (j & 1u) * kPcRawU4 + lane, c, step);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // raw slot read before it is refilled
-        p2_dma(c, step + 4, raw_lds, j & 1u);
-        expand_store_wk<0>(w, ring + (step % kP2Ring) * kPcSlotU4 + lane, kPcLanes);
-      }
-      if (second && step < nsteps) expand_store_wk<1>(w, ring + (step % kP2Ring) * kPcSlotU4 + lane, kPcLanes);
-      PC_STAMP(t2);
-      __syncthreads();  // barrier b
-      PC_STAMP(t3);
-      PC_ACC(0, t0, t1);
-      PC_ACC(1, t1, t2);
-      PC_ACC(2, t2, t3);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA outlives the workgroup
-  } else {
-    // ---------------- consumer ----------------
-    Digest s;
-    s.init();
-    for (uint32_t k = 0; k < nsteps; ++k) {
-      PC_STAMP(t0);
-      __syncthreads();  // barrier k: slot k % 3 complete
-      PC_STAMP(t1);
-      if (k < c.total) compress_expanded_wk(s, ring + (k % kP2Ring) * kPcSlotU4 + lane, kPcLanes);
-      PC_STAMP(t2);
-      PC_ACC(0, t0, t1);
-      PC_ACC(1, t1, t2);
-    }
-    if (i < p.n) {
-      uint32_t be[5];
-#pragma unroll
-      for (int k = 0; k < 5; ++k) be[k] = bswap(s.h[k]);
-      if (p.digests) {
-        uint32_t* o = reinterpret_cast<uint32_t*>(p.digests + 20ull * i);
-#pragma unroll
-        for (int k = 0; k < 5; ++k) o[k] = be[k];
-      }
-      if (p.verdicts) {
-        const uint32_t* e = reinterpret_cast<const uint32_t*>(p.expected + 20ull * i);
-        uint32_t diff = 0;
-#pragma unroll
-        for (int k = 0; k < 5; ++k) diff |= be[k] ^ e[k];
-        p.verdicts[i] = diff == 0 ? 1 : 0;
-      }
-    }
-  }
-#ifdef LBF_PC_STAMPS
-  if (lane == 0) {
-    unsigned long long* o = g_pc_stamps + (blockIdx.x * 3 + wave) * 4;
-    o[0] = acc[0];
-    o[1] = acc[1];
-    o[2] = acc[2];
-    o[3] = nsteps;
-  }
-#endif
-}
-#endif  // LBF_EXPERIMENTAL_VARIANTS
-
 // ---------------------------------------------------------------------------
-// Kernel "pc4" (variant 6): pc2 with the schedule double-buffered in the
-// consumer's registers.
+// Kernel "pc4" (variant 7): two producers per 64 chains, with the schedule
+// double-buffered in the consumer's registers.
 //
-// pc2's consumer loads step k's 80 words after barrier k and its first round
+// The consumer's round is cheapest (five VALU ops issued back to back) when
+// its schedule word already carries the round constant; adding K costs more
+// than one producer wave has to spare, so two producers alternate steps, each
+// spending two barrier intervals on one (words 0..39, then 40..79).  In the
+// form this grew out of (pc2, tools/experimental/) the consumer loaded step k's 80 words after barrier k and its first round
 // waits for the first of them: an LDS round trip per step, longer while the
 // producers' writes and DMA share the LDS.  Here the producers run one step
 // further ahead (step k+1 is complete at barrier k), and right after barrier k
@@ -333,75 +78,21 @@ __global__ void __launch_bounds__(192) sha1_pc2_kernel(ChunkParams p) {
 // workgroup per CU, so each of the three waves has a SIMD of its own.
 // ---------------------------------------------------------------------------
 constexpr int kPc4Ring = 4;
-// Diagnostic builds only (tools/probe_pc.hip): LBF_PC4_NOLOADS feeds the
-// rounds opaque registers instead of LDS words, LBF_PC4_NOBARRIER drops the
-// barriers.  Both give wrong digests; they isolate what loads and barriers cost.
-#ifdef LBF_PC4_NOLOADS
-#define PC4_LOAD(dst, src) asm volatile("" : "=v"((dst).x), "=v"((dst).y), "=v"((dst).z), "=v"((dst).w))
-#else
-#define PC4_LOAD(dst, src) (dst) = (src)
-#endif
+// Diagnostic builds only (tools/probe_pc.hip): LBF_PC4_NOBARRIER drops the
+// barriers (wrong digests; it isolates what the barriers cost).
 #ifdef LBF_PC4_NOBARRIER
 #define PC4_SYNC() do {} while (0)
 #else
 #define PC4_SYNC() __syncthreads()
 #endif
 constexpr int kPc4LdsBytes = (kPc4Ring * kPcSlotU4 + 2 * kP2Raw * kPcRawU4) * 16;
-constexpr int kPc4Early = 15;  // loads issued before the first round
-constexpr int kPc4LateAt = 3;  // the rest after quad 3's rounds
 
-#ifdef LBF_EXPERIMENTAL_VARIANTS  // not shipped: the uint4 form of pc4 (variant 6)
-// Step from `cur` (in registers); meanwhile the next step's 20 quads are
-// loaded from `next_slot` (this lane's column) into `nxt`.  Every lane runs
-// the rounds (no divergent branch around the late loads); a lane whose chain
-// has ended (`live` false) keeps its digest.
-__device__ __forceinline__ void pc4_compress(Digest& s, const uint4 (&cur)[kPcQuads], uint4 (&nxt)[kPcQuads],
-                                             const uint4* next_slot, bool live, bool all_live) {
-#pragma unroll
-  for (int q = 0; q < kPc4Early; ++q) PC4_LOAD(nxt[q], next_slot[q * kPcLanes]);
-  // early loads go first (fenced on the digest, not on copies of it, so the
-  // working state needs no register copies)
-  asm volatile("" : "+v"(s.h[0]), "+v"(s.h[1]), "+v"(s.h[2]), "+v"(s.h[3]), "+v"(s.h[4])::"memory");
-  uint32_t a = s.h[0], b = s.h[1], c = s.h[2], d = s.h[3], e = s.h[4];
-#pragma unroll
-  for (int q = 0; q < kPcQuads; ++q) {
-    round_step_wk(4 * q + 0, a, b, c, d, e, cur[q].x);
-    round_step_wk(4 * q + 1, a, b, c, d, e, cur[q].y);
-    round_step_wk(4 * q + 2, a, b, c, d, e, cur[q].z);
-    round_step_wk(4 * q + 3, a, b, c, d, e, cur[q].w);
-    if (q == kPc4LateAt) {
-      // The two fences pin the late loads between quads 3 and 4: rounds are
-      // ordered through the state, loads through the memory clobber (left
-      // alone, the compiler sinks them to the end of the step, right before
-      // the barrier, which then waits for them).
-      asm volatile("" : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+v"(e)::"memory");
-#pragma unroll
-      for (int r = kPc4Early; r < kPcQuads; ++r) PC4_LOAD(nxt[r], next_slot[r * kPcLanes]);
-      asm volatile("" : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+v"(e)::"memory");
-    }
-  }
-  if (all_live) {  // wave-uniform: every chain of the workgroup has this step
-    s.h[0] += a;
-    s.h[1] += b;
-    s.h[2] += c;
-    s.h[3] += d;
-    s.h[4] += e;
-  } else {
-    s.h[0] = live ? s.h[0] + a : s.h[0];
-    s.h[1] = live ? s.h[1] + b : s.h[1];
-    s.h[2] = live ? s.h[2] + c : s.h[2];
-    s.h[3] = live ? s.h[3] + d : s.h[3];
-    s.h[4] = live ? s.h[4] + e : s.h[4];
-  }
-}
-#endif  // LBF_EXPERIMENTAL_VARIANTS
-
-// pc4_compress with the schedule read as 40 ds_read_b64 (variant 7).  A lone
+// One consumer step with the schedule read as 40 ds_read_b64 (variant 7).  A lone
 // wave pays ≈96 cycles per block for 20 ds_read_b128 over the same rounds fed
 // from registers, and ≈4 for 40 ds_read_b64 (tools/probe_lds_lanes.hip,
 // profiles/r01/probe_lds_lanes.log).  The lgkm counter holds 15, so the next
 // step's 40 pairs go out in three batches: before round 0, after round 16 and
-// after round 40, each pinned by fences like the late loads of pc4_compress.
+// after round 40, each batch pinned between the rounds by fences.
 // Even batch sizes (14, 14, 12) let the compiler pair every load into a
 // ds_read2st64_b64: 20 LDS instructions per step instead of 21 with (15, 13,
 // 12) -- 0.1 %, inside the noise (profiles/r02/pc4_even_batches/).
@@ -455,25 +146,12 @@ __device__ __forceinline__ void pc5_compress(Digest& s, const uint2 (&cur)[kPc5P
   }
 }
 
-// The consumer's side of one pc4 step in either layout: uint4 quads (kVec 4,
-// variant 6) or uint2 pairs (kVec 2, variant 7) of the same 20 KiB slot.
+// The consumer's side of one pc4 step: the 20 KiB slot read as uint2 pairs
+// (kVec 2, shipped; loads may pair up into ds_read2st64_b64).  kVec 1 keeps
+// every load a single ds_read_b64 and kVec 4 reads uint4 quads: both are
+// superseded forms, specialised in tools/experimental/.
 template <int kVec>
-struct Pc4Sched;
-#ifdef LBF_EXPERIMENTAL_VARIANTS
-template <>
-struct Pc4Sched<4> {
-  uint4 v[kPcQuads];
-  static __device__ __forceinline__ const uint4* col(const uint4* ring, int slot, int lane) {
-    return ring + slot * kPcSlotU4 + lane;
-  }
-  __device__ __forceinline__ void load_all(const uint4* src) {
-#pragma unroll
-    for (int q = 0; q < kPcQuads; ++q) v[q] = src[q * kPcLanes];
-  }
-};
-#endif
-template <int kVec>
-struct Pc4Sched {  // kVec 2: uint2 pairs, loads may pair up; kVec 1: single ds_read_b64 each
+struct Pc4Sched {
   uint2 v[kPc5Pairs];
   static __device__ __forceinline__ const uint2* col(const uint4* ring, int slot, int lane) {
     return reinterpret_cast<const uint2*>(ring + slot * kPcSlotU4) + lane;
@@ -483,12 +161,6 @@ struct Pc4Sched {  // kVec 2: uint2 pairs, loads may pair up; kVec 1: single ds_
     for (int q = 0; q < kPc5Pairs; ++q) v[q] = src[q * kPcLanes];
   }
 };
-#ifdef LBF_EXPERIMENTAL_VARIANTS
-__device__ __forceinline__ void pc4_step(Digest& s, const Pc4Sched<4>& cur, Pc4Sched<4>& nxt, const uint4* next_slot,
-                                         bool live, bool all_live) {
-  pc4_compress(s, cur.v, nxt.v, next_slot, live, all_live);
-}
-#endif
 template <int kVec>
 __device__ __forceinline__ void pc4_step(Digest& s, const Pc4Sched<kVec>& cur, Pc4Sched<kVec>& nxt,
                                          const uint2* next_slot, bool live, bool all_live) {
@@ -526,17 +198,11 @@ __device__ __forceinline__ void pc4_barrier(Digest& s PC4_ACC_ARGS) {
 }
 
 // kUnroll: steps per fast-loop iteration.  Eight since round 3: 0.3-1.1 %
-// faster than four at C2 in alternating runs (profiles/r03/pc4x2/diag/sweep_7_16_*.jsonl);
-// four is experimental variant 16, for A/B.
-// kPrioP0, kPrioP1: wave priority of producer 0 / producer 1 (waves 1 and 2),
-// template parameters only in the experimental build (variants 29-33); the
-// shipped build has the constants 0 below, so its kernel is unchanged.
-#ifdef LBF_EXPERIMENTAL_VARIANTS
-template <bool kUniform, int kVec, int kUnroll = 8, int kPrioP0 = 0, int kPrioP1 = 0>
-#else
-constexpr int kPrioP0 = 0, kPrioP1 = 0;
+// faster than four at C2 in alternating runs (profiles/r03/pc4x2/diag/sweep_7_16_*.jsonl).
+// The producers run at the default wave priority: raising either one's
+// (s_setprio 1-3) measured 0.1-0.5 %, below the box-to-box noise
+// (profiles/r03/pc4x2/prio/).
 template <bool kUniform, int kVec, int kUnroll = 8>
-#endif
 __global__ void __launch_bounds__(192) sha1_pc4_kernel(ChunkParams p) {
   extern __shared__ __attribute__((aligned(16))) uint4 ring[];  // W[3][20][64] | raw[2][2][4][64]
   const int lane = threadIdx.x & 63;
@@ -554,8 +220,6 @@ __global__ void __launch_bounds__(192) sha1_pc4_kernel(ChunkParams p) {
   if (wave != 0) {
     // ---------------- producer X = wave - 1: steps X, X+2, ... ----------------
     const uint32_t X = wave - 1;
-    if (kPrioP0 != 0 && X == 0) __builtin_amdgcn_s_setprio(kPrioP0);
-    if (kPrioP1 != 0 && X == 1) __builtin_amdgcn_s_setprio(kPrioP1);
     uint4* raw = ring + kPc4Ring * kPcSlotU4 + X * (kP2Raw * kPcRawU4);
     const uint32_t raw_lds = (uint32_t)reinterpret_cast<uintptr_t>(raw);
     p2_dma(c, X, raw_lds, 0);
@@ -846,15 +510,6 @@ template <bool kUniform>
 __global__ void __launch_bounds__(384) sha1_pc4x2_kernel(ChunkParams p) {
   pc4x2_body<kUniform, 2, true, kPc4x2Ring, false, 6, true, 0, 1>(p);
 }
-
-#ifdef LBF_EXPERIMENTAL_VARIANTS
-// Diagnostic forms (experimental variants 13-15, 17-19, 21).
-template <bool kUniform, int kGroups, bool kFast, int kRawAt, bool kFence, int kUnroll6, bool kPrio = false,
-          int kPrioG0 = 0, int kPrioG1 = 0>
-__global__ void __launch_bounds__(192 * kGroups) sha1_pc4x2_diag_kernel(ChunkParams p) {
-  pc4x2_body<kUniform, kGroups, kFast, kRawAt, kFence, kUnroll6, kPrio, kPrioG0, kPrioG1>(p);
-}
-#endif
 
 }  // namespace
 }  // namespace lbf

@@ -1,6 +1,6 @@
 // kern_pcx.hpp -- two producer/consumer pairs per workgroup pinned to its
-// CU, one producer each, for 16 K-32 K chains (C4 per GPU): "pcx5" (10) is
-// shipped, "pcx4" (9) is built only with LBF_EXPERIMENTAL_VARIANTS.
+// CU, one producer each, for 16 K-32 K chains: "pcx5" (10), kept for A/B
+// against pc4x2 (12); the "pcx4" (9) it grew out of is in tools/experimental/.
 //
 // Part of the single translation unit sha1_kernels.hip (included from there);
 // DESIGN.md §4 has the measurements behind each kernel.
@@ -37,8 +37,6 @@ namespace {
 // producer, issued 4 steps ahead.
 // ---------------------------------------------------------------------------
 constexpr int kPx4Ring = 2;
-constexpr int kPx4PairU4 = kPx4Ring * kPcSlotU4 + kPcRawSlots * kPcRawU4;  // 56 KiB per pair
-constexpr int kPx4LdsBytes = 2 * kPx4PairU4 * 16;                           // 112 KiB
 
 template <int kKFrom>
 __device__ __forceinline__ void px4_round(int i, uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d, uint32_t& e,
@@ -46,159 +44,6 @@ __device__ __forceinline__ void px4_round(int i, uint32_t& a, uint32_t& b, uint3
   if (i < kKFrom) round_step_kv(i, a, b, c, d, e, x, K);
   else round_step_wk(i, a, b, c, d, e, x);
 }
-
-#ifdef LBF_EXPERIMENTAL_VARIANTS  // not shipped: pcx4 (9), superseded by pcx5
-template <int kKFrom>
-__device__ __forceinline__ void px4_compress(Digest& s, const uint2 (&cur)[kPc5Pairs], uint2 (&nxt)[kPc5Pairs],
-                                             const uint2* next_slot, const RoundK& K, bool live, bool all_live) {
-#pragma unroll
-  for (int q = 0; q < kPc5B1; ++q) nxt[q] = next_slot[q * kPcLanes];
-  asm volatile("" : "+v"(s.h[0]), "+v"(s.h[1]), "+v"(s.h[2]), "+v"(s.h[3]), "+v"(s.h[4])::"memory");
-  uint32_t a = s.h[0], b = s.h[1], c = s.h[2], d = s.h[3], e = s.h[4];
-#pragma unroll
-  for (int q = 0; q < kPc5Pairs; ++q) {
-    px4_round<kKFrom>(2 * q + 0, a, b, c, d, e, cur[q].x, K);
-    px4_round<kKFrom>(2 * q + 1, a, b, c, d, e, cur[q].y, K);
-    if (q == kPc5B1At || q == kPc5B2At) {
-      asm volatile("" : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+v"(e)::"memory");
-      const int lo = q == kPc5B1At ? kPc5B1 : kPc5B2;
-      const int hi = q == kPc5B1At ? kPc5B2 : kPc5Pairs;
-#pragma unroll
-      for (int r = lo; r < hi; ++r) nxt[r] = next_slot[r * kPcLanes];
-      asm volatile("" : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+v"(e)::"memory");
-    }
-  }
-  if (all_live) {
-    s.h[0] += a;
-    s.h[1] += b;
-    s.h[2] += c;
-    s.h[3] += d;
-    s.h[4] += e;
-  } else {
-    s.h[0] = live ? s.h[0] + a : s.h[0];
-    s.h[1] = live ? s.h[1] + b : s.h[1];
-    s.h[2] = live ? s.h[2] + c : s.h[2];
-    s.h[3] = live ? s.h[3] + d : s.h[3];
-    s.h[4] = live ? s.h[4] + e : s.h[4];
-  }
-}
-
-// One whole step of this producer's 64 chains into ring slot step % 2; the
-// raw slot it read is refilled with block step + 4.
-template <int kKFrom>
-__device__ __forceinline__ void px4_produce(uint4* ring, uint32_t raw_lds, const ChainInfo& c, uint32_t step,
-                                            int lane) {
-  uint32_t w[16];
-  asm volatile("s_waitcnt vmcnt(12)" ::: "memory");  // block `step` landed; steps +1..+3 pending
-  const uint4* raw = ring + kPx4Ring * kPcSlotU4 + (step % kPcRawSlots) * kPcRawU4 + lane;
-  if (step < c.nfull) {
-    if (c.aligned) {
-      block_from_vec(w, raw[0], raw[kPcLanes], raw[2 * kPcLanes], raw[3 * kPcLanes]);
-    } else {
-      load_words_any(w, c.src + 64ull * step, 64);
-#pragma unroll
-      for (int k = 0; k < 16; ++k) w[k] = bswap(w[k]);
-    }
-  } else {
-    final_block(w, c.src + 64ull * c.nfull, c.size & 63u, c.size, step != c.nfull);
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // raw slot read before it is refilled
-  pc_dma_step(c, step + kPcRawSlots, raw_lds);
-  expand_store_split<kKFrom>(w, reinterpret_cast<uint2*>(ring + (step % kPx4Ring) * kPcSlotU4) + lane, kPcLanes);
-}
-
-template <bool kUniform, int kKFrom>
-__global__ void __launch_bounds__(256) sha1_pcx4_kernel(ChunkParams p) {
-  extern __shared__ __attribute__((aligned(16))) uint4 lds_all[];  // per pair: W[2][20][64] | raw[4][4][64]
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int pair = wave & 1;
-  uint4* ring = lds_all + pair * kPx4PairU4;
-  const uint32_t i = blockIdx.x * (2 * kPcLanes) + pair * kPcLanes + lane;
-  const ChainInfo c = chain_info<kUniform>(p, i);
-  // every wave passes every barrier: the step count is the workgroup's maximum
-  __shared__ uint32_t wg_steps;
-  if (threadIdx.x == 0) wg_steps = 0;
-  __syncthreads();
-  const uint32_t mine = __builtin_amdgcn_readfirstlane(wave_max(c.total));
-  if (lane == 0) atomicMax(&wg_steps, mine);
-  __syncthreads();
-  const uint32_t nsteps = __builtin_amdgcn_readfirstlane(wg_steps);
-  if (nsteps == 0) return;  // uniform over the workgroup: no barrier is left waiting
-
-  if (wave >= 2) {
-    // ---------------- producer ----------------
-    const uint32_t raw_lds = (uint32_t)reinterpret_cast<uintptr_t>(ring + kPx4Ring * kPcSlotU4);
-#pragma unroll
-    for (uint32_t r = 0; r < (uint32_t)kPcRawSlots; ++r) pc_dma_step(c, r, raw_lds);
-    px4_produce<kKFrom>(ring, raw_lds, c, 0, lane);
-    if (nsteps > 1) px4_produce<kKFrom>(ring, raw_lds, c, 1, lane);
-    __syncthreads();  // barrier P: steps 0 and 1 complete
-    __syncthreads();  // barrier 0: the consumers hold step 0, slot 0 is free
-    for (uint32_t k = 0; k + 1 < nsteps; ++k) {
-      // interval k+1: step k+2 into slot k % 2
-      if (k + 2 < nsteps) px4_produce<kKFrom>(ring, raw_lds, c, k + 2, lane);
-      __syncthreads();  // barrier k+1
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA outlives the workgroup
-  } else {
-    // ---------------- consumer ----------------
-    Digest s;
-    s.init();
-    const RoundK K;
-    Pc4Sched<2> A, B;
-#ifdef LBF_PC_STAMPS
-    unsigned long long acc[4] = {0, 0, 0, 0};
-#define PX4_ACC , acc
-#else
-#define PX4_ACC
-#endif
-    const uint32_t min_steps = __builtin_amdgcn_readfirstlane(wave_min(i < p.n ? c.total : 0xFFFFFFFFu));
-    __syncthreads();  // barrier P
-    A.load_all(Pc4Sched<2>::col(ring, 0, lane));
-    __syncthreads();  // barrier 0 (its fence completes the loads)
-    uint32_t k = 0;
-    // two steps per iteration while every chain of the pair runs and each step
-    // is followed by a barrier: k % 2 == 0, so the slot offsets are immediates
-    for (; k + 2 <= min_steps && k + 2 < nsteps; k += 2) {
-      px4_compress<kKFrom>(s, A.v, B.v, Pc4Sched<2>::col(ring, 1, lane), K, true, true);
-      pc4_barrier(s PX4_ACC);  // barrier k+1
-      px4_compress<kKFrom>(s, B.v, A.v, Pc4Sched<2>::col(ring, 0, lane), K, true, true);
-      pc4_barrier(s PX4_ACC);  // barrier k+2
-    }
-    for (; k < nsteps; k += 2) {
-      px4_compress<kKFrom>(s, A.v, B.v, Pc4Sched<2>::col(ring, (k + 1) % kPx4Ring, lane), K, k < c.total,
-                           k < min_steps);
-      if (k + 1 >= nsteps) break;
-      pc4_barrier(s PX4_ACC);  // barrier k+1
-      px4_compress<kKFrom>(s, B.v, A.v, Pc4Sched<2>::col(ring, k % kPx4Ring, lane), K, k + 1 < c.total,
-                           k + 1 < min_steps);
-      if (k + 2 >= nsteps) break;
-      pc4_barrier(s PX4_ACC);  // barrier k+2
-    }
-    if (i < p.n) write_result(p, i, s);
-#undef PX4_ACC
-  }
-}
-
-// K split: the consumer adds K in rounds 0..39.  Splitting at 20 or 0 ran 5 %
-// slower at every chain count (profiles/r01/sweep_v5_pcx4_ksplit.log).
-constexpr int kPx4KFrom = 40;
-
-template <int kKFrom>
-void launch_pcx4(const ChunkParams& p, hipStream_t stream) {
-  static std::once_flag once;
-  std::call_once(once, [] {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pcx4_kernel<false, kKFrom>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, kPx4LdsBytes);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pcx4_kernel<true, kKFrom>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, kPx4LdsBytes);
-  });
-  const uint32_t blocks = (p.n + 2 * kPcLanes - 1) / (2 * kPcLanes);
-  if (p.offsets) hipLaunchKernelGGL((sha1_pcx4_kernel<false, kKFrom>), dim3(blocks), dim3(256), kPx4LdsBytes, stream, p);
-  else hipLaunchKernelGGL((sha1_pcx4_kernel<true, kKFrom>), dim3(blocks), dim3(256), kPx4LdsBytes, stream, p);
-}
-#endif  // LBF_EXPERIMENTAL_VARIANTS
 
 // ---------------------------------------------------------------------------
 // Kernel "pcx5" (variant 10): pcx4 with the producer's first 16 words left in

@@ -38,4 +38,13 @@ struct ChunkParams {
 int pick_variant(uint64_t n);
 int launch_chunks(const ChunkParams& p, hipStream_t stream);
 
+// Kernel variants beyond the shipped ones (1, 7, 10, 11, 12).  Null in the
+// shipped library; the A/B library of tools/experimental/ points it at its
+// superseded and diagnostic variants when it loads.
+struct ExtraVariants {
+  bool (*known)(int variant);
+  bool (*launch)(int variant, const ChunkParams& p, hipStream_t stream);
+};
+extern const ExtraVariants* g_extra_variants;
+
 }  // namespace lbf

@@ -20,8 +20,9 @@
 //   "lds2" (variant 11): one chunk per lane with LDS-DMA staging of whole
 //     128-byte lines -- many chains (C3).
 // The superseded variants (2 pc, 3 lds, 4 pc2, 5 pcx2, 6 pc4/uint4, 8 pc4/b64
-// single loads, 9 pcx4) are compiled only with -DLBF_EXPERIMENTAL_VARIANTS
-// (`make experimental`), for A/B sweeps (tools/sweep_variants.py).
+// single loads, 9 pcx4) and the diagnostic forms (13-33) are not in this
+// library: tools/experimental/ builds them into an A/B library of its own,
+// which registers them through g_extra_variants (lbf_internal.hpp).
 #include <hip/hip_runtime.h>
 
 #include <atomic>
@@ -65,12 +66,16 @@ __global__ void __launch_bounds__(256) fill_synth_kernel(uint8_t* dst, uint64_t 
 }
 
 std::atomic<int> g_variant{0};
+
+bool shipped_variant(int v) { return v == 1 || v == 7 || v == 10 || v == 11 || v == 12; }
 // Chain counts up to which pc4 / pcx2 are chosen automatically (tuned on
 // MI355X, see DESIGN.md "kernel selection"): 64 chains per CU, 128 per CU.
 constexpr uint32_t kPc4MaxChains = 16384;
 constexpr uint32_t kPcMaxChains = 32768;
 
 }  // namespace
+
+const ExtraVariants* g_extra_variants = nullptr;
 
 int pick_variant(uint64_t n) {
   int variant = g_variant.load();
@@ -102,30 +107,14 @@ int pick_variant(uint64_t n) {
 }
 
 template <bool kUniform>
-void launch_pc4(const ChunkParams& p, hipStream_t stream, int kvec) {
+void launch_pc4(const ChunkParams& p, hipStream_t stream) {
   static std::once_flag once;
   std::call_once(once, [] {
-    for (const void* f : {reinterpret_cast<const void*>(&sha1_pc4_kernel<kUniform, 2>),
-#ifdef LBF_EXPERIMENTAL_VARIANTS
-                          reinterpret_cast<const void*>(&sha1_pc4_kernel<kUniform, 4>),
-                          reinterpret_cast<const void*>(&sha1_pc4_kernel<kUniform, 1>),
-#endif
-                         })
-      (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kPc4LdsBytes);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4_kernel<kUniform, 2>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, kPc4LdsBytes);
   });
-  const dim3 g((p.n + kPcLanes - 1) / kPcLanes), b(192);
-#ifdef LBF_EXPERIMENTAL_VARIANTS
-  if (kvec == 4) {
-    hipLaunchKernelGGL((sha1_pc4_kernel<kUniform, 4>), g, b, kPc4LdsBytes, stream, p);
-    return;
-  }
-  if (kvec == 1) {
-    hipLaunchKernelGGL((sha1_pc4_kernel<kUniform, 1>), g, b, kPc4LdsBytes, stream, p);
-    return;
-  }
-#endif
-  (void)kvec;
-  hipLaunchKernelGGL((sha1_pc4_kernel<kUniform, 2>), g, b, kPc4LdsBytes, stream, p);
+  hipLaunchKernelGGL((sha1_pc4_kernel<kUniform, 2>), dim3((p.n + kPcLanes - 1) / kPcLanes), dim3(192), kPc4LdsBytes,
+                     stream, p);
 }
 
 template <bool kUniform>
@@ -156,241 +145,21 @@ void launch_lane(const ChunkParams& p, hipStream_t stream) {
   hipLaunchKernelGGL(sha1_lane_kernel<kUniform>, dim3((p.n + threads - 1) / threads), dim3(threads), 0, stream, p);
 }
 
-#ifdef LBF_EXPERIMENTAL_VARIANTS
-// pc4x2, consumers at priority 3, producers of group 0 / group 1 at kP0 / kP1
-template <int kP0, int kP1>
-void launch_pc4x2_prio(const ChunkParams& p, hipStream_t stream) {
-  static std::once_flag once;
-  std::call_once(once, [] {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4x2_diag_kernel<false, 2, true, 3, false, 6, true, kP0, kP1>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, kPc4x2LdsBytes);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4x2_diag_kernel<true, 2, true, 3, false, 6, true, kP0, kP1>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, kPc4x2LdsBytes);
-  });
-  const uint32_t blocks = (p.n + 2 * kPcLanes - 1) / (2 * kPcLanes);
-  if (p.offsets) hipLaunchKernelGGL((sha1_pc4x2_diag_kernel<false, 2, true, 3, false, 6, true, kP0, kP1>), dim3(blocks), dim3(384), kPc4x2LdsBytes, stream, p);
-  else hipLaunchKernelGGL((sha1_pc4x2_diag_kernel<true, 2, true, 3, false, 6, true, kP0, kP1>), dim3(blocks), dim3(384), kPc4x2LdsBytes, stream, p);
-}
-
-// pc4 with its producers (waves 1, 2) at wave priorities kP0 / kP1
-template <int kP0, int kP1>
-void launch_pc4_prio(const ChunkParams& p, hipStream_t stream) {
-  static std::once_flag once;
-  std::call_once(once, [] {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4_kernel<false, 2, 8, kP0, kP1>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, kPc4LdsBytes);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4_kernel<true, 2, 8, kP0, kP1>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, kPc4LdsBytes);
-  });
-  const dim3 g((p.n + kPcLanes - 1) / kPcLanes), b(192);
-  if (p.offsets) hipLaunchKernelGGL((sha1_pc4_kernel<false, 2, 8, kP0, kP1>), g, b, kPc4LdsBytes, stream, p);
-  else hipLaunchKernelGGL((sha1_pc4_kernel<true, 2, 8, kP0, kP1>), g, b, kPc4LdsBytes, stream, p);
-}
-
-// Superseded variants, kept for A/B sweeps: false when `variant` is not one.
-bool launch_experimental(int variant, const ChunkParams& p, hipStream_t stream) {
-  if (variant == 2) {
-    const uint32_t blocks = (p.n + kPcLanes - 1) / kPcLanes;
-    constexpr int lds = pc_lds_bytes<2>();
-    if (p.offsets) hipLaunchKernelGGL((sha1_pc_kernel<false, 2>), dim3(blocks), dim3(128), lds, stream, p);
-    else hipLaunchKernelGGL((sha1_pc_kernel<true, 2>), dim3(blocks), dim3(128), lds, stream, p);
-  } else if (variant == 5) {
-    constexpr int lds = 2 * pc_lds_bytes<2>();
-    static std::once_flag once;
-    std::call_once(once, [] {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc_kernel<false, 2, 2>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc_kernel<true, 2, 2>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    });
-    const uint32_t blocks = (p.n + 2 * kPcLanes - 1) / (2 * kPcLanes);
-    if (p.offsets) hipLaunchKernelGGL((sha1_pc_kernel<false, 2, 2>), dim3(blocks), dim3(256), lds, stream, p);
-    else hipLaunchKernelGGL((sha1_pc_kernel<true, 2, 2>), dim3(blocks), dim3(256), lds, stream, p);
-  } else if (variant == 4) {
-    static std::once_flag once;
-    std::call_once(once, [] {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc2_kernel<false>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, kP2LdsBytes);
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc2_kernel<true>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, kP2LdsBytes);
-    });
-    const uint32_t blocks = (p.n + kPcLanes - 1) / kPcLanes;
-    if (p.offsets) hipLaunchKernelGGL(sha1_pc2_kernel<false>, dim3(blocks), dim3(192), kP2LdsBytes, stream, p);
-    else hipLaunchKernelGGL(sha1_pc2_kernel<true>, dim3(blocks), dim3(192), kP2LdsBytes, stream, p);
-  } else if (variant == 6 || variant == 8) {
-    const int kvec = variant == 6 ? 4 : 1;
-    if (p.offsets) launch_pc4<false>(p, stream, kvec);
-    else launch_pc4<true>(p, stream, kvec);
-  } else if (variant == 9) {
-    launch_pcx4<kPx4KFrom>(p, stream);
-  } else if (variant == 13 || variant == 14) {
-    // pc4x2's structure with one group (diagnostics; 14 without the six-step
-    // loop); 100 KiB pins one workgroup per CU
-    constexpr int lds = 100 * 1024;
-    static std::once_flag once;
-    std::call_once(once, [] {
-      for (const void* f : {reinterpret_cast<const void*>(&sha1_pc4x2_diag_kernel<false, 1, true, 3, false, 6>),
-                            reinterpret_cast<const void*>(&sha1_pc4x2_diag_kernel<true, 1, true, 3, false, 6>),
-                            reinterpret_cast<const void*>(&sha1_pc4x2_diag_kernel<false, 1, false, 3, false, 6>),
-                            reinterpret_cast<const void*>(&sha1_pc4x2_diag_kernel<true, 1, false, 3, false, 6>)})
-        (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    });
-    const uint32_t blocks = (p.n + kPcLanes - 1) / kPcLanes;
-    if (variant == 13) {
-      if (p.offsets) hipLaunchKernelGGL((sha1_pc4x2_diag_kernel<false, 1, true, 3, false, 6>), dim3(blocks), dim3(192), lds, stream, p);
-      else hipLaunchKernelGGL((sha1_pc4x2_diag_kernel<true, 1, true, 3, false, 6>), dim3(blocks), dim3(192), lds, stream, p);
-    } else {
-      if (p.offsets) hipLaunchKernelGGL((sha1_pc4x2_diag_kernel<false, 1, false, 3, false, 6>), dim3(blocks), dim3(192), lds, stream, p);
-      else hipLaunchKernelGGL((sha1_pc4x2_diag_kernel<true, 1, false, 3, false, 6>), dim3(blocks), dim3(192), lds, stream, p);
-    }
-  } else if (variant == 16) {
-    // pc4 with its fast loop unrolled by four, the form before round 3 (A/B)
-    static std::once_flag once;
-    std::call_once(once, [] {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4_kernel<false, 2, 4>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, kPc4LdsBytes);
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4_kernel<true, 2, 4>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, kPc4LdsBytes);
-    });
-    const dim3 g((p.n + kPcLanes - 1) / kPcLanes), b(192);
-    if (p.offsets) hipLaunchKernelGGL((sha1_pc4_kernel<false, 2, 4>), g, b, kPc4LdsBytes, stream, p);
-    else hipLaunchKernelGGL((sha1_pc4_kernel<true, 2, 4>), g, b, kPc4LdsBytes, stream, p);
-  } else if (variant == 17) {
-    // variant 13 with pc4's LDS layout: raw slots after four W slots (diagnostic)
-    constexpr int lds = 100 * 1024;
-    static std::once_flag once;
-    std::call_once(once, [] {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4x2_diag_kernel<false, 1, true, 4, false, 6>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4x2_diag_kernel<true, 1, true, 4, false, 6>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    });
-    const uint32_t blocks = (p.n + kPcLanes - 1) / kPcLanes;
-    if (p.offsets) hipLaunchKernelGGL((sha1_pc4x2_diag_kernel<false, 1, true, 4, false, 6>), dim3(blocks), dim3(192), lds, stream, p);
-    else hipLaunchKernelGGL((sha1_pc4x2_diag_kernel<true, 1, true, 4, false, 6>), dim3(blocks), dim3(192), lds, stream, p);
-  } else if (variant == 18 || variant == 19) {
-    // pc4x2 (18) and its one-group form (19) with scheduling barriers around the
-    // producers' workgroup barrier (diagnostics)
-    constexpr int lds1 = 100 * 1024;
-    static std::once_flag once;
-    std::call_once(once, [] {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4x2_diag_kernel<false, 2, true, 3, true, 6>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, kPc4x2LdsBytes);
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4x2_diag_kernel<true, 2, true, 3, true, 6>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, kPc4x2LdsBytes);
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4x2_diag_kernel<false, 1, true, 3, true, 6>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, lds1);
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4x2_diag_kernel<true, 1, true, 3, true, 6>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, lds1);
-    });
-    if (variant == 18) {
-      const uint32_t blocks = (p.n + 2 * kPcLanes - 1) / (2 * kPcLanes);
-      if (p.offsets) hipLaunchKernelGGL((sha1_pc4x2_diag_kernel<false, 2, true, 3, true, 6>), dim3(blocks), dim3(384), kPc4x2LdsBytes, stream, p);
-      else hipLaunchKernelGGL((sha1_pc4x2_diag_kernel<true, 2, true, 3, true, 6>), dim3(blocks), dim3(384), kPc4x2LdsBytes, stream, p);
-    } else {
-      const uint32_t blocks = (p.n + kPcLanes - 1) / kPcLanes;
-      if (p.offsets) hipLaunchKernelGGL((sha1_pc4x2_diag_kernel<false, 1, true, 3, true, 6>), dim3(blocks), dim3(192), lds1, stream, p);
-      else hipLaunchKernelGGL((sha1_pc4x2_diag_kernel<true, 1, true, 3, true, 6>), dim3(blocks), dim3(192), lds1, stream, p);
-    }
-  } else if (variant == 20) {
-    // pc4 with its fast loop unrolled by sixteen (A/B)
-    static std::once_flag once;
-    std::call_once(once, [] {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4_kernel<false, 2, 16>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, kPc4LdsBytes);
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4_kernel<true, 2, 16>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, kPc4LdsBytes);
-    });
-    const dim3 g((p.n + kPcLanes - 1) / kPcLanes), b(192);
-    if (p.offsets) hipLaunchKernelGGL((sha1_pc4_kernel<false, 2, 16>), g, b, kPc4LdsBytes, stream, p);
-    else hipLaunchKernelGGL((sha1_pc4_kernel<true, 2, 16>), g, b, kPc4LdsBytes, stream, p);
-  } else if (variant == 21) {
-    // pc4x2 with its fast loop unrolled by twelve (A/B)
-    static std::once_flag once;
-    std::call_once(once, [] {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4x2_diag_kernel<false, 2, true, 3, false, 12>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, kPc4x2LdsBytes);
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4x2_diag_kernel<true, 2, true, 3, false, 12>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, kPc4x2LdsBytes);
-    });
-    const uint32_t blocks = (p.n + 2 * kPcLanes - 1) / (2 * kPcLanes);
-    if (p.offsets) hipLaunchKernelGGL((sha1_pc4x2_diag_kernel<false, 2, true, 3, false, 12>), dim3(blocks), dim3(384), kPc4x2LdsBytes, stream, p);
-    else hipLaunchKernelGGL((sha1_pc4x2_diag_kernel<true, 2, true, 3, false, 12>), dim3(blocks), dim3(384), kPc4x2LdsBytes, stream, p);
-  } else if (variant == 22 || variant == 23) {
-    // pc4x2 (22) and its one-group form (23) with the consumers at wave priority 3 (diagnostics)
-    constexpr int lds1 = 100 * 1024;
-    static std::once_flag once;
-    std::call_once(once, [] {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4x2_diag_kernel<false, 2, true, 3, false, 6, true>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, kPc4x2LdsBytes);
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4x2_diag_kernel<true, 2, true, 3, false, 6, true>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, kPc4x2LdsBytes);
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4x2_diag_kernel<false, 1, true, 3, false, 6, true>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, lds1);
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4x2_diag_kernel<true, 1, true, 3, false, 6, true>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, lds1);
-    });
-    if (variant == 22) {
-      const uint32_t blocks = (p.n + 2 * kPcLanes - 1) / (2 * kPcLanes);
-      if (p.offsets) hipLaunchKernelGGL((sha1_pc4x2_diag_kernel<false, 2, true, 3, false, 6, true>), dim3(blocks), dim3(384), kPc4x2LdsBytes, stream, p);
-      else hipLaunchKernelGGL((sha1_pc4x2_diag_kernel<true, 2, true, 3, false, 6, true>), dim3(blocks), dim3(384), kPc4x2LdsBytes, stream, p);
-    } else {
-      const uint32_t blocks = (p.n + kPcLanes - 1) / kPcLanes;
-      if (p.offsets) hipLaunchKernelGGL((sha1_pc4x2_diag_kernel<false, 1, true, 3, false, 6, true>), dim3(blocks), dim3(192), lds1, stream, p);
-      else hipLaunchKernelGGL((sha1_pc4x2_diag_kernel<true, 1, true, 3, false, 6, true>), dim3(blocks), dim3(192), lds1, stream, p);
-    }
-  } else if (variant >= 29 && variant <= 33) {
-    // pc4 with producer priorities (producer 0, producer 1): 29 (0, 1), 30 (1, 0), 31 (1, 1), 32 (2, 2), 33 (3, 3)
-    if (variant == 29) launch_pc4_prio<0, 1>(p, stream);
-    else if (variant == 30) launch_pc4_prio<1, 0>(p, stream);
-    else if (variant == 31) launch_pc4_prio<1, 1>(p, stream);
-    else if (variant == 32) launch_pc4_prio<2, 2>(p, stream);
-    else launch_pc4_prio<3, 3>(p, stream);
-  } else if (variant >= 25 && variant <= 28) {
-    // pc4x2 (consumers at priority 3) with its producers at wave priorities (group 0, group 1): 25 (0, 1) is the
-    // shipped variant 12's code since session 32, kept so the A/B of profiles/r03/pc4x2/prio/s31_* can be rerun;
-    // 26 (1, 0), 27 (0, 2), 28 (1, 2)
-    if (variant == 25) launch_pc4x2_prio<0, 1>(p, stream);
-    else if (variant == 26) launch_pc4x2_prio<1, 0>(p, stream);
-    else if (variant == 27) launch_pc4x2_prio<0, 2>(p, stream);
-    else launch_pc4x2_prio<1, 2>(p, stream);
-  } else if (variant == 15) {
-    // pc4x2 without the six-step loop (diagnostic)
-    static std::once_flag once;
-    std::call_once(once, [] {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4x2_diag_kernel<false, 2, false, 3, false, 6>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, kPc4x2LdsBytes);
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sha1_pc4x2_diag_kernel<true, 2, false, 3, false, 6>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, kPc4x2LdsBytes);
-    });
-    const uint32_t blocks = (p.n + 2 * kPcLanes - 1) / (2 * kPcLanes);
-    if (p.offsets) hipLaunchKernelGGL((sha1_pc4x2_diag_kernel<false, 2, false, 3, false, 6>), dim3(blocks), dim3(384), kPc4x2LdsBytes, stream, p);
-    else hipLaunchKernelGGL((sha1_pc4x2_diag_kernel<true, 2, false, 3, false, 6>), dim3(blocks), dim3(384), kPc4x2LdsBytes, stream, p);
-  } else if (variant == 3) {
-    const uint32_t blocks = (p.n + 255) / 256;
-    constexpr int lds = 4 * kLdsStages * kPcRawU4 * 16;
-    if (p.offsets) hipLaunchKernelGGL((sha1_lds_kernel<false, kLdsStages>), dim3(blocks), dim3(256), lds, stream, p);
-    else hipLaunchKernelGGL((sha1_lds_kernel<true, kLdsStages>), dim3(blocks), dim3(256), lds, stream, p);
-  } else {
-    return false;
-  }
-  return true;
-}
-#endif
 
 int launch_chunks(const ChunkParams& p, hipStream_t stream) {
   if (p.n == 0) return LBF_OK;
   const int variant = pick_variant(p.n);
   const bool uniform = p.offsets == nullptr;
-#ifdef LBF_EXPERIMENTAL_VARIANTS
-  if (launch_experimental(variant, p, stream)) {
+  if (!shipped_variant(variant)) {
+    // a variant only an A/B library registers (lbf_set_kernel_variant accepted it)
+    if (!g_extra_variants || !g_extra_variants->launch(variant, p, stream))
+      return fail(LBF_ERR_INVALID, "kernel variant " + std::to_string(variant) + " has no launcher");
     LBF_HIP_TRY(hipGetLastError());
     return LBF_OK;
   }
-#endif
   if (variant == 7) {
-    if (uniform) launch_pc4<true>(p, stream, 2);
-    else launch_pc4<false>(p, stream, 2);
+    if (uniform) launch_pc4<true>(p, stream);
+    else launch_pc4<false>(p, stream);
   } else if (variant == 10) {
     launch_pcx5<kPx5KFrom>(p, stream);
   } else if (variant == 12) {
@@ -399,7 +168,7 @@ int launch_chunks(const ChunkParams& p, hipStream_t stream) {
   } else if (variant == 11) {
     if (uniform) launch_lds2<true>(p, stream);
     else launch_lds2<false>(p, stream);
-  } else {
+  } else {  // 1
     if (uniform) launch_lane<true>(p, stream);
     else launch_lane<false>(p, stream);
   }
@@ -464,11 +233,8 @@ extern "C" int lbf_sha1_uniform_launch(const uint8_t* d_base, uint64_t len, uint
 }
 
 extern "C" int lbf_set_kernel_variant(int variant) {
-#ifdef LBF_EXPERIMENTAL_VARIANTS
-  const bool known = variant >= 0 && variant <= 33;
-#else
-  const bool known = variant == 0 || variant == 1 || variant == 7 || variant == 10 || variant == 11 || variant == 12;
-#endif
+  const bool known = variant == 0 || lbf::shipped_variant(variant) ||
+                     (lbf::g_extra_variants && lbf::g_extra_variants->known(variant));
   if (!known) return fail(LBF_ERR_INVALID, "unknown kernel variant (shipped: 0 auto, 1, 7, 10, 11, 12)");
   lbf::g_variant.store(variant);
   return LBF_OK;

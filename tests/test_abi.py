@@ -77,7 +77,7 @@ def test_no_gpu_fails_loudly():
 
 def test_shipped_kernel_variants_only():
     """The product library carries the five shipped kernels (1 lane, 7 pc4/b64,
-    10 pcx5, 11 lds2, 12 pc4x2); the superseded ones exist only in the experimental build."""
+    10 pcx5, 11 lds2, 12 pc4x2); the superseded ones exist only in the A/B library of tools/experimental/."""
     lib = _capi.load()
     try:
         for v in (0, 1, 7, 10, 11, 12):

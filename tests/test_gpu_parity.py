@@ -28,8 +28,8 @@ SEED_C = 0x5EED
 # 16-32 K chains until round 3), 11 = one chunk per lane with LDS-DMA staging
 # of whole 128-byte lines ("lds2", many chains), 12 = two pc4 groups in one
 # 6-wave workgroup, producers two to a SIMD ("pc4x2", 16-32 K chains since
-# round 3).  The superseded variants live only in
-# the experimental build (make -C bitflood_amd/csrc experimental).
+# round 3).  The superseded variants live only in the A/B library of
+# tools/experimental/ (make -C tools/experimental).
 VARIANTS = [1, 7, 10, 11, 12]
 
 

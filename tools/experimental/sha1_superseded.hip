@@ -1,0 +1,683 @@
+// tools/experimental/sha1_superseded.hip -- the superseded and diagnostic
+// chunk-hash kernels, for A/B runs against the shipped ones.  NOT product code:
+// nothing here is in bitflood_amd/lib/liblbfhash.so.
+//
+// `make -C tools/experimental` links this translation unit with the shipped
+// objects (bitflood_amd/lib/sha1_kernels.o, lbf_capi.o) into
+// tools/build/experimental/liblbfhash.so; at load time it points
+// lbf::g_extra_variants at the table below, so lbf_set_kernel_variant accepts
+// these variants and launch_chunks launches them.  Tools select the library
+// with LBF_LIB=tools/build/experimental/liblbfhash.so (tools/sweep_variants.py).
+// tools/probe_pc.hip includes this file after the shipped sources (one TU).
+//
+// Variants (DESIGN.md §4 has what each one measured):
+//    2 pc       one consumer + one producer per 64 chains, W ring of 2 slots
+//    3 lds      one chunk per lane, one 64-byte block per LDS-DMA step
+//    4 pc2      one consumer + two producers, consumer loads after each barrier
+//    5 pcx2     two pc pairs per workgroup
+//    6 pc4      schedule read as uint4 quads
+//    8 pc4      schedule read as single ds_read_b64
+//    9 pcx4     two pairs, K split at round 40, one producer per consumer
+//   13-15, 17-19, 21-23  pc4x2 diagnostics (one group, no six-step loop, LDS
+//              layout, scheduling fences, twelve-step loop, consumer priority)
+//   16, 20    pc4 with its fast loop unrolled by four / sixteen
+//   25-28     pc4x2 producer priorities (25 = the shipped variant 12's code)
+// (The pc4 producer-priority variants 29-33 of round 3 measured 0.1-0.5 %,
+// below the noise, and are not rebuilt.)
+#include <hip/hip_runtime.h>
+
+#include <mutex>
+#include <set>
+
+#include "lbf_internal.hpp"
+#include "kern_common.hpp"
+#include "kern_lane.hpp"
+#include "kern_pc.hpp"
+#include "kern_pcx.hpp"
+
+namespace lbf {
+namespace {
+
+// ---------------------------------------------------------------------------
+// Kernel "pc" (variant 2): producer/consumer split for few chains.
+//
+// With few chunks (C2: 16,384 chains = 256 waves for 1,024 SIMDs) a lone wave
+// issues at most one VALU every ~4 cycles (tools/probe_issue.hip), so the time
+// per chunk is set by the instruction count of ONE chain.  The 64-word message
+// expansion and the byte swaps do not depend on the chain state, so a producer
+// wave on another SIMD computes them and hands the 80 expanded words per block
+// over in LDS; the consumer wave runs only the 80 rounds (5 VALU each).
+//
+// One workgroup = 64 chains = 2 waves: wave 0 consumes, wave 1 produces.  The
+// LDS ring has 2 slots of [20 uint4][64 lanes] (20 KiB each); one workgroup
+// barrier per block step separates "producer writes slot k+1" from "consumer
+// reads slot k".  The producer keeps kPcPrefetch blocks of raw chunk bytes in
+// flight in registers.  Final (padding/length) blocks are built by the
+// producer as ordinary steps, so the consumer loop is uniform.
+// ---------------------------------------------------------------------------
+// Raw bytes of block `step` of every chain into raw slot step % 4, laid out
+// [16-byte piece j][lane] so both the DMA and the later ds_read_b128 are
+// contiguous across lanes.  Always exactly 4 VMEM instructions.
+__device__ __forceinline__ void pc_dma_step(const ChainInfo& c, uint32_t step, uint32_t raw_lds) {
+  const bool ok = c.aligned && step < c.nfull;
+  const uint8_t* src = ok ? c.src + 64ull * step : reinterpret_cast<const uint8_t*>(g_pc_dummy);
+  const uint32_t slot = raw_lds + (step % kPcRawSlots) * (kPcRawU4 * 16);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) dma16(src + 16 * j, slot + j * (kPcLanes * 16));
+}
+
+template <int kRing>
+__device__ __forceinline__ void pc_produce(uint4* ring, const ChainInfo& c, uint32_t step, int lane) {
+  uint32_t w[16];
+  if (step < c.nfull) {
+    if (c.aligned) {
+      const uint4* raw = ring + kRing * kPcSlotU4 + (step % kPcRawSlots) * kPcRawU4 + lane;
+      block_from_vec(w, raw[0], raw[kPcLanes], raw[2 * kPcLanes], raw[3 * kPcLanes]);
+    } else {
+      load_words_any(w, c.src + 64ull * step, 64);
+#pragma unroll
+      for (int k = 0; k < 16; ++k) w[k] = bswap(w[k]);
+    }
+  } else {
+    // step == nfull: block with the tail bytes; step == nfull + 1: zeros + length.
+    // Steps past `total` produce don't-care words the consumer never reads.
+    final_block(w, c.src + 64ull * c.nfull, c.size & 63u, c.size, step != c.nfull);
+  }
+  expand_store(w, ring + (step % kRing) * kPcSlotU4 + lane, kPcLanes);
+}
+
+// kRing = 2 (the shipped form): the producer writes step k+1 into slot
+// (k+1) % 2 while the consumer computes step k from slot k % 2.  A 3-slot ring
+// that let the consumer prefetch step k+1 across the barrier measured 6 % slower
+// (extra VGPR traffic and LDS instructions inside the round chain).
+// kPairs consumer/producer pairs per workgroup (waves 0..kPairs-1 consume,
+// kPairs..2*kPairs-1 produce; pair q = wave % kPairs).  kPairs = 2 with 112 KiB
+// of LDS pins ONE workgroup per CU, so each of its 4 waves has a SIMD to itself
+// -- for 16 K-32 K chains, where two 2- or 3-wave workgroups per CU would put
+// a consumer and a producer on one SIMD.
+template <bool kUniform, int kRing, int kPairs = 1>
+__global__ void __launch_bounds__(128 * kPairs) sha1_pc_kernel(ChunkParams p) {
+  extern __shared__ __attribute__((aligned(16))) uint4 lds_all[];  // per pair: W[kRing][20][64] | raw[4][4][64]
+  const int lane = threadIdx.x & 63;
+  const int wave_id = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int pair = wave_id % kPairs;
+  const int wave = wave_id / kPairs;  // 0 = consumer, 1 = producer
+  uint4* ring = lds_all + pair * (pc_lds_bytes<kRing>() / 16);
+  const uint32_t i = blockIdx.x * (kPcLanes * kPairs) + pair * kPcLanes + lane;
+  const ChainInfo c = chain_info<kUniform>(p, i);
+  // Identical in every wave of the workgroup (every wave passes every
+  // barrier); readfirstlane keeps the loop bounds scalar.
+  uint32_t nsteps = __builtin_amdgcn_readfirstlane(wave_max(c.total));
+  if (kPairs > 1) {
+    __shared__ uint32_t wg_steps;
+    if (threadIdx.x == 0) wg_steps = 0;
+    __syncthreads();
+    if (lane == 0) atomicMax(&wg_steps, nsteps);
+    __syncthreads();
+    nsteps = __builtin_amdgcn_readfirstlane(wg_steps);
+  }
+  const uint32_t nbarriers = nsteps;  // both waves pass exactly nsteps barriers
+  constexpr uint32_t kAhead = kRing - 1;  // steps the producer runs ahead
+#ifdef LBF_PC_STAMPS
+  unsigned long long acc[4] = {0, 0, 0, 0}, t0 = 0, t1 = 0, t2 = 0, t3 = 0;
+#endif
+
+  if (wave == 1) {
+    // ---------------- producer ----------------
+    const uint32_t raw_lds = (uint32_t)reinterpret_cast<uintptr_t>(ring + kRing * kPcSlotU4);
+#pragma unroll
+    for (uint32_t s = 0; s < kPcRawSlots; ++s) pc_dma_step(c, s, raw_lds);
+    // steps 0 .. kAhead-1 before the first barrier, then step k + kAhead in interval k
+    for (uint32_t k = 0; k < nbarriers + kAhead - 1; ++k) {
+      if (k < nsteps) {
+        PC_STAMP(t0);
+        // raw block k has landed once at most the 3 younger steps (12 DMAs) are pending
+        asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+        PC_STAMP(t1);
+        pc_produce<kRing>(ring, c, k, lane);
+        pc_dma_step(c, k + kPcRawSlots, raw_lds);  // reuses slot k % 4 (read above)
+        PC_STAMP(t2);
+        PC_ACC(0, t0, t1);
+        PC_ACC(1, t1, t2);
+      }
+      PC_STAMP(t2);
+      if (k + 1 >= kAhead) __syncthreads();       // barrier (k + 1 - kAhead)
+      PC_STAMP(t3);
+      PC_ACC(2, t2, t3);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA outlives the workgroup
+  } else {
+    // ---------------- consumer ----------------
+    Digest s;
+    s.init();
+    const RoundK K;
+    for (uint32_t k = 0; k < nsteps; ++k) {
+      PC_STAMP(t0);
+      __syncthreads();  // barrier k: slot k % 2 complete
+      PC_STAMP(t1);
+      if (k < c.total) compress_expanded(s, ring + (k % kRing) * kPcSlotU4 + lane, kPcLanes, K);
+      PC_STAMP(t2);
+      PC_ACC(0, t0, t1);
+      PC_ACC(1, t1, t2);
+    }
+    if (i < p.n) {
+      uint32_t be[5];
+#pragma unroll
+      for (int k = 0; k < 5; ++k) be[k] = bswap(s.h[k]);
+      if (p.digests) {
+        uint32_t* o = reinterpret_cast<uint32_t*>(p.digests + 20ull * i);
+#pragma unroll
+        for (int k = 0; k < 5; ++k) o[k] = be[k];
+      }
+      if (p.verdicts) {
+        const uint32_t* e = reinterpret_cast<const uint32_t*>(p.expected + 20ull * i);
+        uint32_t diff = 0;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) diff |= be[k] ^ e[k];
+        p.verdicts[i] = diff == 0 ? 1 : 0;
+      }
+    }
+  }
+#ifdef LBF_PC_STAMPS
+  if (lane == 0) {
+    unsigned long long* o = g_pc_stamps + (blockIdx.x * 2 * kPairs + wave_id) * 4;
+    o[0] = acc[0];
+    o[1] = acc[1];
+    o[2] = acc[2];
+    o[3] = nsteps;
+  }
+#endif
+}
+
+// ---------------------------------------------------------------------------
+// Kernel "pc2" (variant 4): one consumer, TWO producers per 64 chains.
+//
+// The consumer's round is cheapest (five VALU ops issued back to back) when
+// its schedule word already carries the round constant, leaving one v_add_u32
+// and one v_add3_u32 for the sum.  Adding K costs the producer 80 more ops per
+// block, more than one producer wave has to spare, so two producers alternate
+// blocks: producer X builds steps X, X+2, X+4, ... and spends two barrier
+// intervals on each (words 0..39 before the first, 40..79 before the second).
+// W ring: 3 slots (step k in slot k % 3): a slot is rewritten only after the
+// consumer has passed the barrier that ends its read.  Raw staging: 2 slots of
+// 4 KiB per producer.  LDS 76 KiB -> two workgroups per CU.
+// ---------------------------------------------------------------------------
+constexpr int kP2Ring = 3;
+constexpr int kP2LdsBytes = (kP2Ring * kPcSlotU4 + 2 * kP2Raw * kPcRawU4) * 16;
+
+template <bool kUniform>
+__global__ void __launch_bounds__(192) sha1_pc2_kernel(ChunkParams p) {
+  extern __shared__ __attribute__((aligned(16))) uint4 ring[];  // W[3][20][64] | raw[2][2][4][64]
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t i = blockIdx.x * kPcLanes + lane;
+  const ChainInfo c = chain_info<kUniform>(p, i);
+  const uint32_t nsteps = __builtin_amdgcn_readfirstlane(wave_max(c.total));
+#ifdef LBF_PC_STAMPS
+  unsigned long long acc[4] = {0, 0, 0, 0}, t0 = 0, t1 = 0, t2 = 0, t3 = 0;
+#endif
+
+  if (wave != 0) {
+    // ---------------- producer X = wave - 1: steps X, X+2, ... ----------------
+    const uint32_t X = wave - 1;
+    uint4* raw = ring + kP2Ring * kPcSlotU4 + X * (kP2Raw * kPcRawU4);
+    const uint32_t raw_lds = (uint32_t)reinterpret_cast<uintptr_t>(raw);
+    p2_dma(c, X, raw_lds, 0);
+    p2_dma(c, X + 2, raw_lds, 1);
+    uint32_t w[16];
+    // Interval b ends at barrier b.  Producer X finishes step b when b % 2 == X
+    // and starts step b + 1 otherwise; producer 0 builds step 0 whole.
+    for (uint32_t b = 0; b < nsteps; ++b) {
+      const bool second = (b & 1u) == X;
+      const uint32_t step = second ? b : b + 1;
+      const bool first_too = (b == 0 && X == 0);
+      PC_STAMP(t0);
+      PC_COPY(t1, t0);
+      if ((!second || first_too) && step < nsteps) {
+        const uint32_t j = (step - X) >> 1;  // this producer's j-th step
+        // block j has landed once only block j+1's 4 DMAs may be pending
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        PC_STAMP(t1);
+        p2_block(w, raw + (j & 1u) * kPcRawU4 + lane, c, step);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // raw slot read before it is refilled
+        p2_dma(c, step + 4, raw_lds, j & 1u);
+        expand_store_wk<0>(w, ring + (step % kP2Ring) * kPcSlotU4 + lane, kPcLanes);
+      }
+      if (second && step < nsteps) expand_store_wk<1>(w, ring + (step % kP2Ring) * kPcSlotU4 + lane, kPcLanes);
+      PC_STAMP(t2);
+      __syncthreads();  // barrier b
+      PC_STAMP(t3);
+      PC_ACC(0, t0, t1);
+      PC_ACC(1, t1, t2);
+      PC_ACC(2, t2, t3);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA outlives the workgroup
+  } else {
+    // ---------------- consumer ----------------
+    Digest s;
+    s.init();
+    for (uint32_t k = 0; k < nsteps; ++k) {
+      PC_STAMP(t0);
+      __syncthreads();  // barrier k: slot k % 3 complete
+      PC_STAMP(t1);
+      if (k < c.total) compress_expanded_wk(s, ring + (k % kP2Ring) * kPcSlotU4 + lane, kPcLanes);
+      PC_STAMP(t2);
+      PC_ACC(0, t0, t1);
+      PC_ACC(1, t1, t2);
+    }
+    if (i < p.n) {
+      uint32_t be[5];
+#pragma unroll
+      for (int k = 0; k < 5; ++k) be[k] = bswap(s.h[k]);
+      if (p.digests) {
+        uint32_t* o = reinterpret_cast<uint32_t*>(p.digests + 20ull * i);
+#pragma unroll
+        for (int k = 0; k < 5; ++k) o[k] = be[k];
+      }
+      if (p.verdicts) {
+        const uint32_t* e = reinterpret_cast<const uint32_t*>(p.expected + 20ull * i);
+        uint32_t diff = 0;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) diff |= be[k] ^ e[k];
+        p.verdicts[i] = diff == 0 ? 1 : 0;
+      }
+    }
+  }
+#ifdef LBF_PC_STAMPS
+  if (lane == 0) {
+    unsigned long long* o = g_pc_stamps + (blockIdx.x * 3 + wave) * 4;
+    o[0] = acc[0];
+    o[1] = acc[1];
+    o[2] = acc[2];
+    o[3] = nsteps;
+  }
+#endif
+}
+
+// Diagnostic builds only (tools/probe_pc.hip): LBF_PC4_NOLOADS feeds the
+// uint4 form's rounds opaque registers instead of LDS words (wrong digests; it
+// isolates what the loads cost).
+#ifdef LBF_PC4_NOLOADS
+#define PC4_LOAD(dst, src) asm volatile("" : "=v"((dst).x), "=v"((dst).y), "=v"((dst).z), "=v"((dst).w))
+#else
+#define PC4_LOAD(dst, src) (dst) = (src)
+#endif
+constexpr int kPc4Early = 15;  // loads issued before the first round
+constexpr int kPc4LateAt = 3;  // the rest after quad 3's rounds
+
+// ---------------------------------------------------------------------------
+// pc4 with the schedule read as uint4 quads (variant 6): 15 ds_read_b128 go out
+// before the first round and five more after the fourth quad of rounds.
+// ---------------------------------------------------------------------------
+// Step from `cur` (in registers); meanwhile the next step's 20 quads are
+// loaded from `next_slot` (this lane's column) into `nxt`.  Every lane runs
+// the rounds (no divergent branch around the late loads); a lane whose chain
+// has ended (`live` false) keeps its digest.
+__device__ __forceinline__ void pc4_compress(Digest& s, const uint4 (&cur)[kPcQuads], uint4 (&nxt)[kPcQuads],
+                                             const uint4* next_slot, bool live, bool all_live) {
+#pragma unroll
+  for (int q = 0; q < kPc4Early; ++q) PC4_LOAD(nxt[q], next_slot[q * kPcLanes]);
+  // early loads go first (fenced on the digest, not on copies of it, so the
+  // working state needs no register copies)
+  asm volatile("" : "+v"(s.h[0]), "+v"(s.h[1]), "+v"(s.h[2]), "+v"(s.h[3]), "+v"(s.h[4])::"memory");
+  uint32_t a = s.h[0], b = s.h[1], c = s.h[2], d = s.h[3], e = s.h[4];
+#pragma unroll
+  for (int q = 0; q < kPcQuads; ++q) {
+    round_step_wk(4 * q + 0, a, b, c, d, e, cur[q].x);
+    round_step_wk(4 * q + 1, a, b, c, d, e, cur[q].y);
+    round_step_wk(4 * q + 2, a, b, c, d, e, cur[q].z);
+    round_step_wk(4 * q + 3, a, b, c, d, e, cur[q].w);
+    if (q == kPc4LateAt) {
+      // The two fences pin the late loads between quads 3 and 4: rounds are
+      // ordered through the state, loads through the memory clobber (left
+      // alone, the compiler sinks them to the end of the step, right before
+      // the barrier, which then waits for them).
+      asm volatile("" : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+v"(e)::"memory");
+#pragma unroll
+      for (int r = kPc4Early; r < kPcQuads; ++r) PC4_LOAD(nxt[r], next_slot[r * kPcLanes]);
+      asm volatile("" : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+v"(e)::"memory");
+    }
+  }
+  if (all_live) {  // wave-uniform: every chain of the workgroup has this step
+    s.h[0] += a;
+    s.h[1] += b;
+    s.h[2] += c;
+    s.h[3] += d;
+    s.h[4] += e;
+  } else {
+    s.h[0] = live ? s.h[0] + a : s.h[0];
+    s.h[1] = live ? s.h[1] + b : s.h[1];
+    s.h[2] = live ? s.h[2] + c : s.h[2];
+    s.h[3] = live ? s.h[3] + d : s.h[3];
+    s.h[4] = live ? s.h[4] + e : s.h[4];
+  }
+}
+
+template <>
+struct Pc4Sched<4> {
+  uint4 v[kPcQuads];
+  static __device__ __forceinline__ const uint4* col(const uint4* ring, int slot, int lane) {
+    return ring + slot * kPcSlotU4 + lane;
+  }
+  __device__ __forceinline__ void load_all(const uint4* src) {
+#pragma unroll
+    for (int q = 0; q < kPcQuads; ++q) v[q] = src[q * kPcLanes];
+  }
+};
+
+__device__ __forceinline__ void pc4_step(Digest& s, const Pc4Sched<4>& cur, Pc4Sched<4>& nxt, const uint4* next_slot,
+                                         bool live, bool all_live) {
+  pc4_compress(s, cur.v, nxt.v, next_slot, live, all_live);
+}
+
+// ---------------------------------------------------------------------------
+// Kernel "lds" (variant 3): one chunk per lane for MANY chains.
+//
+// With >= 4 waves per SIMD the VALU itself is the limit (≈2,040 SIMD cycles per
+// 64-byte block) and what is left to win is memory stall: in the
+// lane kernel the compiler sinks every 16-byte load next to its use, so each
+// block waits a full HBM round trip.  Here each wave streams its 64 chains'
+// next kStages blocks global -> LDS with DMA (no VGPRs in flight, so the
+// compiler cannot move them) and waits by count.  LDS per wave: kStages x 4 KiB.
+// ---------------------------------------------------------------------------
+template <int kStages>
+__device__ __forceinline__ void lds_dma_step(const ChainInfo& c, uint32_t step, uint32_t wave_lds) {
+  const bool ok = c.aligned && step < c.nfull;
+  const uint8_t* src = ok ? c.src + 64ull * step : reinterpret_cast<const uint8_t*>(g_pc_dummy);
+  const uint32_t slot = wave_lds + (step % kStages) * (kPcRawU4 * 16);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) dma16(src + 16 * j, slot + j * (kPcLanes * 16));
+}
+
+template <bool kUniform, int kStages>
+__global__ void __launch_bounds__(256) sha1_lds_kernel(ChunkParams p) {
+  extern __shared__ __attribute__((aligned(16))) uint4 stage[];  // [wave][kStages][4][64]
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const ChainInfo c = chain_info<kUniform>(p, i);
+  uint4* mine = stage + wave * (kStages * kPcRawU4);
+  const uint32_t wave_lds = (uint32_t)reinterpret_cast<uintptr_t>(mine);
+  const uint32_t nsteps = __builtin_amdgcn_readfirstlane(wave_max(c.nfull));
+  const bool any_unaligned = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(__ballot(c.total != 0 && !c.aligned) != 0));
+  Digest s;
+  s.init();
+#pragma unroll
+  for (uint32_t k = 0; k < (uint32_t)kStages; ++k) lds_dma_step<kStages>(c, k, wave_lds);
+  for (uint32_t k = 0; k < nsteps; ++k) {
+    // block k has landed once at most the (kStages-1) younger steps are pending
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (kStages - 1)) : "memory");
+    const uint4* raw = mine + (k % kStages) * kPcRawU4 + lane;
+    uint32_t w[16];
+    block_from_vec(w, raw[0], raw[kPcLanes], raw[2 * kPcLanes], raw[3 * kPcLanes]);
+    if (any_unaligned && !c.aligned && k < c.nfull) {
+      load_words_any(w, c.src + 64ull * k, 64);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) w[q] = bswap(w[q]);
+    }
+    // the slot is refilled below: its ds_reads must have returned first
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    lds_dma_step<kStages>(c, k + kStages, wave_lds);
+    if (k < c.nfull) compress(s, w);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA outlives the wave
+  if (i >= p.n) return;
+  finish(s, c.src + 64ull * c.nfull, c.size & 63u, c.size);
+  uint32_t be[5];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) be[k] = bswap(s.h[k]);
+  if (p.digests) {
+    uint32_t* o = reinterpret_cast<uint32_t*>(p.digests + 20ull * i);
+#pragma unroll
+    for (int k = 0; k < 5; ++k) o[k] = be[k];
+  }
+  if (p.verdicts) {
+    const uint32_t* e = reinterpret_cast<const uint32_t*>(p.expected + 20ull * i);
+    uint32_t diff = 0;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) diff |= be[k] ^ e[k];
+    p.verdicts[i] = diff == 0 ? 1 : 0;
+  }
+}
+constexpr int kLdsStages = 2;
+
+// ---------------------------------------------------------------------------
+// Kernel "pcx4" (variant 9): see kern_pcx.hpp for the design pcx5 keeps.
+// ---------------------------------------------------------------------------
+constexpr int kPx4PairU4 = kPx4Ring * kPcSlotU4 + kPcRawSlots * kPcRawU4;  // 56 KiB per pair
+constexpr int kPx4LdsBytes = 2 * kPx4PairU4 * 16;                           // 112 KiB
+
+template <int kKFrom>
+__device__ __forceinline__ void px4_compress(Digest& s, const uint2 (&cur)[kPc5Pairs], uint2 (&nxt)[kPc5Pairs],
+                                             const uint2* next_slot, const RoundK& K, bool live, bool all_live) {
+#pragma unroll
+  for (int q = 0; q < kPc5B1; ++q) nxt[q] = next_slot[q * kPcLanes];
+  asm volatile("" : "+v"(s.h[0]), "+v"(s.h[1]), "+v"(s.h[2]), "+v"(s.h[3]), "+v"(s.h[4])::"memory");
+  uint32_t a = s.h[0], b = s.h[1], c = s.h[2], d = s.h[3], e = s.h[4];
+#pragma unroll
+  for (int q = 0; q < kPc5Pairs; ++q) {
+    px4_round<kKFrom>(2 * q + 0, a, b, c, d, e, cur[q].x, K);
+    px4_round<kKFrom>(2 * q + 1, a, b, c, d, e, cur[q].y, K);
+    if (q == kPc5B1At || q == kPc5B2At) {
+      asm volatile("" : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+v"(e)::"memory");
+      const int lo = q == kPc5B1At ? kPc5B1 : kPc5B2;
+      const int hi = q == kPc5B1At ? kPc5B2 : kPc5Pairs;
+#pragma unroll
+      for (int r = lo; r < hi; ++r) nxt[r] = next_slot[r * kPcLanes];
+      asm volatile("" : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+v"(e)::"memory");
+    }
+  }
+  if (all_live) {
+    s.h[0] += a;
+    s.h[1] += b;
+    s.h[2] += c;
+    s.h[3] += d;
+    s.h[4] += e;
+  } else {
+    s.h[0] = live ? s.h[0] + a : s.h[0];
+    s.h[1] = live ? s.h[1] + b : s.h[1];
+    s.h[2] = live ? s.h[2] + c : s.h[2];
+    s.h[3] = live ? s.h[3] + d : s.h[3];
+    s.h[4] = live ? s.h[4] + e : s.h[4];
+  }
+}
+
+// One whole step of this producer's 64 chains into ring slot step % 2; the
+// raw slot it read is refilled with block step + 4.
+template <int kKFrom>
+__device__ __forceinline__ void px4_produce(uint4* ring, uint32_t raw_lds, const ChainInfo& c, uint32_t step,
+                                            int lane) {
+  uint32_t w[16];
+  asm volatile("s_waitcnt vmcnt(12)" ::: "memory");  // block `step` landed; steps +1..+3 pending
+  const uint4* raw = ring + kPx4Ring * kPcSlotU4 + (step % kPcRawSlots) * kPcRawU4 + lane;
+  if (step < c.nfull) {
+    if (c.aligned) {
+      block_from_vec(w, raw[0], raw[kPcLanes], raw[2 * kPcLanes], raw[3 * kPcLanes]);
+    } else {
+      load_words_any(w, c.src + 64ull * step, 64);
+#pragma unroll
+      for (int k = 0; k < 16; ++k) w[k] = bswap(w[k]);
+    }
+  } else {
+    final_block(w, c.src + 64ull * c.nfull, c.size & 63u, c.size, step != c.nfull);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // raw slot read before it is refilled
+  pc_dma_step(c, step + kPcRawSlots, raw_lds);
+  expand_store_split<kKFrom>(w, reinterpret_cast<uint2*>(ring + (step % kPx4Ring) * kPcSlotU4) + lane, kPcLanes);
+}
+
+template <bool kUniform, int kKFrom>
+__global__ void __launch_bounds__(256) sha1_pcx4_kernel(ChunkParams p) {
+  extern __shared__ __attribute__((aligned(16))) uint4 lds_all[];  // per pair: W[2][20][64] | raw[4][4][64]
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int pair = wave & 1;
+  uint4* ring = lds_all + pair * kPx4PairU4;
+  const uint32_t i = blockIdx.x * (2 * kPcLanes) + pair * kPcLanes + lane;
+  const ChainInfo c = chain_info<kUniform>(p, i);
+  // every wave passes every barrier: the step count is the workgroup's maximum
+  __shared__ uint32_t wg_steps;
+  if (threadIdx.x == 0) wg_steps = 0;
+  __syncthreads();
+  const uint32_t mine = __builtin_amdgcn_readfirstlane(wave_max(c.total));
+  if (lane == 0) atomicMax(&wg_steps, mine);
+  __syncthreads();
+  const uint32_t nsteps = __builtin_amdgcn_readfirstlane(wg_steps);
+  if (nsteps == 0) return;  // uniform over the workgroup: no barrier is left waiting
+
+  if (wave >= 2) {
+    // ---------------- producer ----------------
+    const uint32_t raw_lds = (uint32_t)reinterpret_cast<uintptr_t>(ring + kPx4Ring * kPcSlotU4);
+#pragma unroll
+    for (uint32_t r = 0; r < (uint32_t)kPcRawSlots; ++r) pc_dma_step(c, r, raw_lds);
+    px4_produce<kKFrom>(ring, raw_lds, c, 0, lane);
+    if (nsteps > 1) px4_produce<kKFrom>(ring, raw_lds, c, 1, lane);
+    __syncthreads();  // barrier P: steps 0 and 1 complete
+    __syncthreads();  // barrier 0: the consumers hold step 0, slot 0 is free
+    for (uint32_t k = 0; k + 1 < nsteps; ++k) {
+      // interval k+1: step k+2 into slot k % 2
+      if (k + 2 < nsteps) px4_produce<kKFrom>(ring, raw_lds, c, k + 2, lane);
+      __syncthreads();  // barrier k+1
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA outlives the workgroup
+  } else {
+    // ---------------- consumer ----------------
+    Digest s;
+    s.init();
+    const RoundK K;
+    Pc4Sched<2> A, B;
+#ifdef LBF_PC_STAMPS
+    unsigned long long acc[4] = {0, 0, 0, 0};
+#define PX4_ACC , acc
+#else
+#define PX4_ACC
+#endif
+    const uint32_t min_steps = __builtin_amdgcn_readfirstlane(wave_min(i < p.n ? c.total : 0xFFFFFFFFu));
+    __syncthreads();  // barrier P
+    A.load_all(Pc4Sched<2>::col(ring, 0, lane));
+    __syncthreads();  // barrier 0 (its fence completes the loads)
+    uint32_t k = 0;
+    // two steps per iteration while every chain of the pair runs and each step
+    // is followed by a barrier: k % 2 == 0, so the slot offsets are immediates
+    for (; k + 2 <= min_steps && k + 2 < nsteps; k += 2) {
+      px4_compress<kKFrom>(s, A.v, B.v, Pc4Sched<2>::col(ring, 1, lane), K, true, true);
+      pc4_barrier(s PX4_ACC);  // barrier k+1
+      px4_compress<kKFrom>(s, B.v, A.v, Pc4Sched<2>::col(ring, 0, lane), K, true, true);
+      pc4_barrier(s PX4_ACC);  // barrier k+2
+    }
+    for (; k < nsteps; k += 2) {
+      px4_compress<kKFrom>(s, A.v, B.v, Pc4Sched<2>::col(ring, (k + 1) % kPx4Ring, lane), K, k < c.total,
+                           k < min_steps);
+      if (k + 1 >= nsteps) break;
+      pc4_barrier(s PX4_ACC);  // barrier k+1
+      px4_compress<kKFrom>(s, B.v, A.v, Pc4Sched<2>::col(ring, k % kPx4Ring, lane), K, k + 1 < c.total,
+                           k + 1 < min_steps);
+      if (k + 2 >= nsteps) break;
+      pc4_barrier(s PX4_ACC);  // barrier k+2
+    }
+    if (i < p.n) write_result(p, i, s);
+#undef PX4_ACC
+  }
+}
+
+// K split: the consumer adds K in rounds 0..39.  Splitting at 20 or 0 ran 5 %
+// slower at every chain count (profiles/r01/sweep_v5_pcx4_ksplit.log).
+constexpr int kPx4KFrom = 40;
+
+// pc4x2 diagnostic forms (variants 13-15, 17-19, 21-23, 25-28);
+// the template parameters are documented at pc4x2_body (kern_pc.hpp).
+// Diagnostic forms (experimental variants 13-15, 17-19, 21).
+template <bool kUniform, int kGroups, bool kFast, int kRawAt, bool kFence, int kUnroll6, bool kPrio = false,
+          int kPrioG0 = 0, int kPrioG1 = 0>
+__global__ void __launch_bounds__(192 * kGroups) sha1_pc4x2_diag_kernel(ChunkParams p) {
+  pc4x2_body<kUniform, kGroups, kFast, kRawAt, kFence, kUnroll6, kPrio, kPrioG0, kPrioG1>(p);
+}
+
+// ---------------------------------------------------------------------------
+// The launch table
+// ---------------------------------------------------------------------------
+using Kern = void (*)(ChunkParams);
+
+struct Entry {
+  int variant;
+  Kern ragged, uniform;      // offsets/sizes table, uniform chunking
+  uint32_t chains_per_wg, threads;
+  int lds_bytes;
+};
+
+constexpr int kDiagLds1 = 100 * 1024;  // one pc4x2 group: 100 KiB pins one workgroup per CU
+
+const Entry kTable[] = {
+    {2, &sha1_pc_kernel<false, 2>, &sha1_pc_kernel<true, 2>, 64, 128, pc_lds_bytes<2>()},
+    {3, &sha1_lds_kernel<false, kLdsStages>, &sha1_lds_kernel<true, kLdsStages>, 256, 256,
+     4 * kLdsStages * kPcRawU4 * 16},
+    {4, &sha1_pc2_kernel<false>, &sha1_pc2_kernel<true>, 64, 192, kP2LdsBytes},
+    {5, &sha1_pc_kernel<false, 2, 2>, &sha1_pc_kernel<true, 2, 2>, 128, 256, 2 * pc_lds_bytes<2>()},
+    {6, &sha1_pc4_kernel<false, 4>, &sha1_pc4_kernel<true, 4>, 64, 192, kPc4LdsBytes},
+    {8, &sha1_pc4_kernel<false, 1>, &sha1_pc4_kernel<true, 1>, 64, 192, kPc4LdsBytes},
+    {9, &sha1_pcx4_kernel<false, kPx4KFrom>, &sha1_pcx4_kernel<true, kPx4KFrom>, 128, 256, kPx4LdsBytes},
+    {13, &sha1_pc4x2_diag_kernel<false, 1, true, 3, false, 6>, &sha1_pc4x2_diag_kernel<true, 1, true, 3, false, 6>,
+     64, 192, kDiagLds1},
+    {14, &sha1_pc4x2_diag_kernel<false, 1, false, 3, false, 6>, &sha1_pc4x2_diag_kernel<true, 1, false, 3, false, 6>,
+     64, 192, kDiagLds1},
+    {15, &sha1_pc4x2_diag_kernel<false, 2, false, 3, false, 6>, &sha1_pc4x2_diag_kernel<true, 2, false, 3, false, 6>,
+     128, 384, kPc4x2LdsBytes},
+    {16, &sha1_pc4_kernel<false, 2, 4>, &sha1_pc4_kernel<true, 2, 4>, 64, 192, kPc4LdsBytes},
+    {17, &sha1_pc4x2_diag_kernel<false, 1, true, 4, false, 6>, &sha1_pc4x2_diag_kernel<true, 1, true, 4, false, 6>,
+     64, 192, kDiagLds1},
+    {18, &sha1_pc4x2_diag_kernel<false, 2, true, 3, true, 6>, &sha1_pc4x2_diag_kernel<true, 2, true, 3, true, 6>,
+     128, 384, kPc4x2LdsBytes},
+    {19, &sha1_pc4x2_diag_kernel<false, 1, true, 3, true, 6>, &sha1_pc4x2_diag_kernel<true, 1, true, 3, true, 6>,
+     64, 192, kDiagLds1},
+    {20, &sha1_pc4_kernel<false, 2, 16>, &sha1_pc4_kernel<true, 2, 16>, 64, 192, kPc4LdsBytes},
+    {21, &sha1_pc4x2_diag_kernel<false, 2, true, 3, false, 12>, &sha1_pc4x2_diag_kernel<true, 2, true, 3, false, 12>,
+     128, 384, kPc4x2LdsBytes},
+    {22, &sha1_pc4x2_diag_kernel<false, 2, true, 3, false, 6, true>,
+     &sha1_pc4x2_diag_kernel<true, 2, true, 3, false, 6, true>, 128, 384, kPc4x2LdsBytes},
+    {23, &sha1_pc4x2_diag_kernel<false, 1, true, 3, false, 6, true>,
+     &sha1_pc4x2_diag_kernel<true, 1, true, 3, false, 6, true>, 64, 192, kDiagLds1},
+    {25, &sha1_pc4x2_diag_kernel<false, 2, true, 3, false, 6, true, 0, 1>,
+     &sha1_pc4x2_diag_kernel<true, 2, true, 3, false, 6, true, 0, 1>, 128, 384, kPc4x2LdsBytes},
+    {26, &sha1_pc4x2_diag_kernel<false, 2, true, 3, false, 6, true, 1, 0>,
+     &sha1_pc4x2_diag_kernel<true, 2, true, 3, false, 6, true, 1, 0>, 128, 384, kPc4x2LdsBytes},
+    {27, &sha1_pc4x2_diag_kernel<false, 2, true, 3, false, 6, true, 0, 2>,
+     &sha1_pc4x2_diag_kernel<true, 2, true, 3, false, 6, true, 0, 2>, 128, 384, kPc4x2LdsBytes},
+    {28, &sha1_pc4x2_diag_kernel<false, 2, true, 3, false, 6, true, 1, 2>,
+     &sha1_pc4x2_diag_kernel<true, 2, true, 3, false, 6, true, 1, 2>, 128, 384, kPc4x2LdsBytes},
+};
+
+const Entry* find_entry(int variant) {
+  for (const Entry& e : kTable)
+    if (e.variant == variant) return &e;
+  return nullptr;
+}
+
+bool superseded_known(int variant) { return find_entry(variant) != nullptr; }
+
+bool superseded_launch(int variant, const ChunkParams& p, hipStream_t stream) {
+  const Entry* e = find_entry(variant);
+  if (!e) return false;
+  const Kern k = p.offsets ? e->ragged : e->uniform;
+  {
+    // dynamic LDS above 64 KiB needs the attribute, once per kernel
+    static std::mutex mu;
+    static std::set<Kern> done;
+    std::lock_guard<std::mutex> lock(mu);
+    if (done.insert(k).second)
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                e->lds_bytes);
+  }
+  ChunkParams q = p;
+  void* args[] = {&q};
+  const uint32_t blocks = (p.n + e->chains_per_wg - 1) / e->chains_per_wg;
+  return hipLaunchKernel(reinterpret_cast<const void*>(k), dim3(blocks), dim3(e->threads), args, e->lds_bytes,
+                         stream) == hipSuccess;
+}
+
+const ExtraVariants kSuperseded = {&superseded_known, &superseded_launch};
+// Registered when the library (or a tool that includes this file) loads.
+const bool kRegistered = (g_extra_variants = &kSuperseded, true);
+
+}  // namespace
+}  // namespace lbf

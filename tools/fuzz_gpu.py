@@ -27,8 +27,8 @@ from bitflood_amd import ChunkHasher, DeviceBuffer  # noqa: E402
 from bitflood_amd import hashing as H  # noqa: E402
 from tests.oracle_lib import Oracle  # noqa: E402
 
-# Shipped variants; with LBF_LIB pointing at the experimental build
-# (make -C bitflood_amd/csrc experimental) LBF_FUZZ_ALL=1 adds the rest.
+# Shipped variants; with LBF_LIB pointing at the A/B library of
+# tools/experimental/ (make -C tools/experimental) LBF_FUZZ_ALL=1 adds the rest.
 VARIANTS = list(range(1, 13)) if os.environ.get("LBF_FUZZ_ALL") else [1, 7, 10, 11, 12]
 THREADS = min(16, os.cpu_count() or 1)
 

@@ -1,10 +1,11 @@
 // tools/probe_pc.hip -- diagnostic build of the pc kernel with s_memtime stamps
 // (not product code).  Compiles the product sources with LBF_PC_STAMPS and
 // prints, per role, the mean cycles per block step spent waiting vs working.
-// Build: hipcc --offload-arch=gfx950 -O3 -DLBF_PC_STAMPS -DLBF_EXPERIMENTAL_VARIANTS -I../include -I../bitflood_amd/csrc \
+// Build: hipcc --offload-arch=gfx950 -O3 -DLBF_PC_STAMPS -I../include -I../bitflood_amd/csrc \
 //          probe_pc.hip -o build/probe_pc
 #include "../bitflood_amd/csrc/lbf_capi.cpp"
 #include "../bitflood_amd/csrc/sha1_kernels.hip"
+#include "experimental/sha1_superseded.hip"  // variants 4, 6, 13
 
 #include <stdio.h>
 #include <vector>

@@ -6,9 +6,9 @@ several chunk counts and chunk sizes over one device-resident synthetic region,
 including the C3 shape (64 GiB at 256 KiB = 262,144 chunks) and the per-GPU C4
 shape (32 GiB at 1 MiB = 32,768 chunks).  Prints one JSON line per point.
 Usage: python tools/sweep_variants.py [--max-gib 64] [--reps 3]
-Superseded variants (2-6, 8, 9) need the experimental build:
-  make -C bitflood_amd/csrc experimental
-  LBF_LIB=bitflood_amd/lib/experimental/liblbfhash.so python tools/sweep_variants.py --variants 4,7
+Superseded and diagnostic variants (2-6, 8, 9, 13-23, 25-28) need the A/B library:
+  make -C tools/experimental
+  LBF_LIB=tools/build/experimental/liblbfhash.so python tools/sweep_variants.py --variants 4,7
 """
 import argparse
 import hashlib
