@@ -24,6 +24,10 @@ Launch:  python bench.py [--gpus N --steps K --warmup W] [--config c2|c4]
    ranks than visible GPUs (rehearsals on a small box) the self-launch uses gloo
    and the line says so (LBF_BENCH_BACKEND overrides).
 
+LBF_BENCH_FORM_GROUP=1 at --gpus 1: rank 0 forms a one-rank process group
+(RCCL unless LBF_BENCH_BACKEND says otherwise) and takes the N>1 route below,
+so every collective of the N-GPU line runs on a 1-GPU box (tests/test_gpu_nccl.py).
+
 N>1 also measures, after the timed region:
   * e2e: every rank hashes (the first 4 GiB of) its shard from host memory at
     the same moment, pageable and then registered, through its own NUMA-local
@@ -31,6 +35,8 @@ N>1 also measures, after the timed region:
   * e2e_inprocess: rank 0 alone, after the others have finished, hashes one
     registered N x 4 GiB host buffer through ONE lbf_ctx over every visible
     device (Encoder::EncodeFile's shape on an N-GPU node).
+At every N rank 0 then times cpu_baseline (the reference encoder's hash on the
+host's usable cores, same stream) once the GPU legs are over.
 """
 import math
 import argparse
@@ -91,6 +97,9 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="0 = every CPU this process may use (affinity, capped by the cgroup CPU quota)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-min-s", type=float, default=3.0,
+                    help="cpu_baseline: seconds each multi-thread rate is timed over (>= 3 s by default, so a cgroup "
+                         "quota's per-period burst cannot inflate it)")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host->device->host rate")
     ap.add_argument("--no-other-configs", action="store_true",
                     help="skip the device-resident C3 and C4 measurements that follow the main line at N=1")
@@ -218,6 +227,26 @@ class _stdout_to_stderr:
         return False
 
 
+def init_group(backend, rank, world, dev):
+    """The process group of one rank: RCCL ("nccl") bound to its device, or gloo.
+    gloo's C++ side prints its "[Gloo] Rank r is connected to ..." notice on
+    stdout, where the launcher collects the one JSON line: while the group
+    forms, the process's stdout points at stderr."""
+    import torch.distributed as dist
+    with _stdout_to_stderr():
+        if backend == "nccl":
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(backend, rank=rank, world_size=world)
+
+
+def grouped():
+    """True while a process group is formed: the collectives below then run
+    through it even at world 1 (LBF_BENCH_FORM_GROUP)."""
+    import torch.distributed as dist
+    return dist.is_available() and dist.is_initialized()
+
+
 def dist_setup(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -230,25 +259,25 @@ def dist_setup(args):
     # one rank per GPU; more ranks than GPUs only for rehearsals of the
     # multi-rank flow on a small box (process group gloo)
     dev = local % ndev
-    if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(dev)
-        backend = os.environ.get("LBF_BENCH_BACKEND", "nccl")
-        # gloo's C++ side prints its "[Gloo] Rank r is connected to ..." notice on
-        # stdout, where the launcher collects the one JSON line: while the group
-        # forms, the process's stdout points at stderr
-        with _stdout_to_stderr():
-            if backend == "nccl":
-                dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", dev))
-            else:
-                dist.init_process_group(backend, rank=rank, world_size=world)
-    else:
-        torch.cuda.set_device(0)
+    torch.cuda.set_device(dev)
+    if world > 1 or os.environ.get("LBF_BENCH_FORM_GROUP") == "1":
+        init_group(os.environ.get("LBF_BENCH_BACKEND", "nccl"), rank, world, dev)
     return rank, world, local, dev, ndev
 
 
+def backend_name():
+    import torch.distributed as dist
+    return str(dist.get_backend())
+
+
+def under_profiler():
+    """A profiler's preloaded library (rocprofv3) is in this process."""
+    pre = os.environ.get("LD_PRELOAD", "")
+    return "rocprof" in pre or any(k.startswith("ROCPROF") for k in os.environ)
+
+
 def barrier(world):
-    if world > 1:
+    if grouped():
         import torch.distributed as dist
         dist.barrier()
 
@@ -335,16 +364,18 @@ def cpu_baseline(args, stream_start, n_chunks_sample, gpu_digests_sample):
 
     # all usable host cores, chunk-parallel; >= 3 s, so a
     # cgroup quota's per-period burst cannot inflate it
-    mt_gibs, reps, d_mt = rate(orc.sha1_batch_unrolled, threads, max_reps=400)
+    min_s = args.cpu_min_s
+    mt_gibs, reps, d_mt = rate(orc.sha1_batch_unrolled, threads, min_s=min_s, max_reps=400)
     # one thread per CPU of the affinity mask (256 on a GPU box): what the quota
     # lets through over the same >= 3 s
-    aff_gibs = (rate(orc.sha1_batch_unrolled, affinity, max_reps=400)[0] if affinity != threads else mt_gibs)
+    aff_gibs = (rate(orc.sha1_batch_unrolled, affinity, min_s=min_s, max_reps=400)[0] if affinity != threads
+                else mt_gibs)
     # one thread, like Encoder.cpp:40-79 (a quarter of the sample)
     n1 = max(1, n_chunks_sample // 4)
     st_gibs, _, d_1 = rate(orc.sha1_batch_unrolled, 1, n=n1, min_s=0.0, max_reps=1)
     clock1 = orc.clock_ghz()
     # the checker's loop form, for continuity with round 1-2 lines
-    loop_mt = rate(orc.sha1_batch, threads, min_s=1.5, max_reps=10)
+    loop_mt = rate(orc.sha1_batch, threads, min_s=min_s / 2, max_reps=10)
     loop_st = rate(orc.sha1_batch, 1, n=n1 // 2 or 1, min_s=0.0, max_reps=1)
     # fread-inclusive single-thread encode of the same bytes as a file, as
     # Encoder::EncodeFile does it (one chunk buffer, fread + hash per chunk);
@@ -371,7 +402,7 @@ def cpu_baseline(args, stream_start, n_chunks_sample, gpu_digests_sample):
         "implementation": "oracle/sha1_unrolled.c: unrolled 80-round Transform in Crypto++ 5.2.1's shape "
                           "(sha.cpp:34-69), gcc -O2, portable C, no SHA-NI",
         "sample": f"{n_chunks_sample} x {cs // 1024} KiB chunks ({nbytes / GIB:.2f} GiB) of the same stream, "
-                  f"passes for >= 3 s on {threads} threads ({reps} passes) and on {affinity}; single-thread pass "
+                  f"passes for >= {min_s:g} s on {threads} threads ({reps} passes) and on {affinity}; single-thread pass "
                   f"over {n1} chunks",
         "usable_threads_value": round(mt_gibs, 3),
         "single_thread_value": round(st_gibs, 3),
@@ -385,7 +416,7 @@ def cpu_baseline(args, stream_start, n_chunks_sample, gpu_digests_sample):
                  "clock_note": "one core, dependent-add chain (oracle unrolled_clock_probe), before and after "
                                "the multi-thread passes"},
         "parity_vs_gpu": parity,
-    }, data
+    }
 
 
 def _host_desc():
@@ -645,7 +676,7 @@ def other_configs():
 
 
 def _gather(x, world, dtype):
-    if world == 1:
+    if not grouped():
         return [x]
     import torch.distributed as dist
     backend = dist.get_backend()
@@ -667,9 +698,16 @@ def gather_floats(x, world):
 def main():
     args = parse()
     if args.gpus > 1 and "RANK" not in os.environ:
+        if under_profiler():
+            # the profiler's preload has initialised the GPU in this process: a
+            # launcher here would start GPU children from it (not allowed)
+            raise SystemExit("bench.py: --gpus N without a launcher starts its own rank processes, which is not "
+                             "allowed under rocprofv3; profile one rank per process instead (torch.distributed.run "
+                             "with rocprofv3 inside each rank, or --gpus 1)")
         # no outside launcher: start the N ranks here (children, never exec)
         sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
     rank, world, local, dev, ndev = dist_setup(args)
+    multi = grouped()  # world > 1, or a one-rank group (LBF_BENCH_FORM_GROUP)
     if args.variant:
         H.set_kernel_variant(args.variant)
     cs = args.chunk_size
@@ -726,14 +764,14 @@ def main():
     e2e_multi = None
     n_slice = min(file_bytes, E2E_SLICE_BYTES) // cs  # whole chunks only
     slice_bytes = n_slice * cs
-    if world > 1:
+    if multi:
         # the host slice, then free the shard's HBM before the host-memory legs:
         # with ranks sharing a GPU (rehearsals: 8 x 32 GiB of C4 on one card)
         # their contexts' device slots would not fit beside it
         host = buf.download(slice_bytes) if not args.no_e2e else None
         buf.free()
         buf = None
-    if world > 1 and not args.no_e2e and n_slice:
+    if multi and not args.no_e2e and n_slice:
         r = e2e_leg(host, cs, dev, world)
         del host
         ok = int(np.array_equal(r["digests"], digests[:n_slice]) and r["registered_equal"])
@@ -759,6 +797,7 @@ def main():
         if r["error"]:
             e2e_multi["error_rank0"] = r["error"]
     slice_hashes = gather_ints(slice_hash(digests[:n_slice]), world)
+    gpu0_numa = None
     shard_starts = [shard_range(world * n_chunks, q, world)[0] * cs for q in range(world)]
 
     variant = H.load().lbf_kernel_for(n_chunks)
@@ -831,7 +870,7 @@ def main():
             },
             "ranks": {
                 "launcher": os.environ.get("LBF_BENCH_LAUNCHER", "torch.distributed.run" if world > 1 else "none"),
-                "process_group": os.environ.get("LBF_BENCH_BACKEND", "nccl") if world > 1 else None,
+                "process_group": backend_name() if multi else None,
                 "visible_gpus": ndev,
                 "device_per_rank": per_rank_dev,
                 "kernel_ms_per_rank": per_rank_kernel_ms,
@@ -843,10 +882,7 @@ def main():
                                     "launches queue on the shared device, so value is not an N-GPU rate")
         if e2e_multi is not None:
             out["e2e"] = e2e_multi
-        if world == 1 and not args.no_cpu_baseline:
-            sample = min(n_chunks, max(1, GIB // cs))
-            cb, host = cpu_baseline(args, stream_start, sample, digests[:sample])
-            out["cpu_baseline"] = cb
+        if not multi:
             if not args.no_e2e:
                 # the whole file, copied back from HBM into pageable host memory
                 host_file = buf.download(file_bytes)
@@ -861,13 +897,13 @@ def main():
                                          "parity": r["registered_equal"]}
                 if r["error"]:
                     out["e2e_error"] = r["error"]
-                cb["host"]["gpu0_numa_node"] = r["placement"]["numa_node"]
+                gpu0_numa = r["placement"]["numa_node"]
         out["first_chunk_b64"] = b64_27(bytes(digests[0]))
-    if world > 1:
+    if multi:
         import torch.distributed as dist
         barrier(world)  # every rank's e2e leg has ended before rank 0 goes on alone
         dist.destroy_process_group()
-    if rank == 0 and world > 1 and not args.no_e2e and not args.no_inproc and n_slice:
+    if rank == 0 and multi and not args.no_e2e and not args.no_inproc and n_slice:
         gen = None
         try:
             gen = DeviceBuffer(slice_bytes)
@@ -880,8 +916,20 @@ def main():
     if buf is not None:
         buf.free()
     dig.free()
-    if rank == 0 and world == 1 and not args.no_other_configs and args.config == "c2":
+    if rank == 0 and not multi and not args.no_other_configs and args.config == "c2":
         out["other_configs"] = other_configs()
+    if rank == 0 and not args.no_cpu_baseline:
+        # at every N, rank 0 alone once the GPU legs are over (the other ranks
+        # have left the group), on the same stream as its shard
+        sample = min(n_chunks, max(1, GIB // cs))
+        cb = cpu_baseline(args, stream_start, sample, digests[:sample])
+        if e2e_multi is not None:
+            gpu0_numa = e2e_multi["numa_per_rank"][0]["numa_node"]
+        if gpu0_numa is not None:
+            cb["host"]["gpu0_numa_node"] = gpu0_numa
+        cb["when"] = ("after the timed region and the host-memory legs, rank 0 alone"
+                      + (f" (ranks 1-{world - 1} have finished)" if world > 1 else ""))
+        out["cpu_baseline"] = cb
     if rank == 0:
         print(json.dumps(out), flush=True)
 

@@ -43,11 +43,14 @@ def gather_digests(local: np.ndarray, n_chunks: int, world: int, group=None) -> 
 
 
 def max_over_ranks(x: float, world: int, group=None) -> float:
-    """The bench's clock: the slowest rank's time."""
-    if world == 1:
+    """The bench's clock: the slowest rank's time (a collective whenever a
+    process group is formed, even of one rank)."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        if world != 1:
+            raise RuntimeError("max_over_ranks: world > 1 without a process group")
         return float(x)
     import torch
-    import torch.distributed as dist
     backend = dist.get_backend(group)
     dev = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
     t = torch.tensor([float(x)], dtype=torch.float64, device=dev)

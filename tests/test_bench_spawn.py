@@ -16,14 +16,15 @@ import bench
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 STUB = os.path.join(ROOT, "tests", "spawn_rank_stub.py")
+FAKE = os.path.join(ROOT, "tests", "bench_fake_rank.py")
 
 
-def _run_spawner(n, env_extra=None, timeout=120):
+def _run_spawner(n, env_extra=None, timeout=120, script=STUB, argv=()):
     """bench.spawn_ranks in a child Python, so its stdout is capturable."""
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LBF_BENCH_BACKEND")}
     env.update(env_extra or {})
     code = (f"import sys; sys.path.insert(0, {ROOT!r}); import bench; "
-            f"sys.exit(bench.spawn_ranks({n}, [], script={STUB!r}))")
+            f"sys.exit(bench.spawn_ranks({n}, {list(argv)!r}, script={script!r}))")
     return subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=timeout,
                           cwd=ROOT)
 
@@ -106,3 +107,66 @@ def test_gloo_connect_notice_stays_off_stdout(tmp_path):
     for r, (out, err) in enumerate(outs):
         assert out.strip() == '{"rank": %d}' % r, out
         assert "[Gloo]" in err
+
+
+# What an N>1 line must carry for the driver's 1/2/4/8-GPU record (VERDICT r03
+# "Next round" #1): the device-resident value with its roofline, the CPU
+# comparator timed in the same run, per-rank golden parity, and both
+# host-memory legs.
+N_LINE_KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+               "vs_baseline", "dtype", "data", "config", "roofline", "compute_floor", "cpu_baseline", "parity",
+               "ranks", "e2e", "e2e_inprocess", "digest_check", "first_chunk_b64"}
+FAKE_ARGV = ["--steps", "2", "--warmup", "1", "--file-gib", "0.0625", "--cpu-min-s", "0.3"]
+
+
+def _check_line(out, n):
+    assert N_LINE_KEYS <= set(out), N_LINE_KEYS - set(out)
+    assert out["n_gpus"] == n and out["scaling"] == "weak" and out["value"] > 0
+    r = out["roofline"]
+    assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 8000.0 and r["achieved"] > 0
+    cb = out["cpu_baseline"]
+    assert cb["kind"] == "port" and cb["unit"] == "GiB/s" and cb["value"] > 0 and cb["cores"] >= 1
+    assert cb["parity_vs_gpu"] is True and cb["host"]["usable_cores"] >= 1
+    assert "rank 0 alone" in cb["when"]
+    assert out["parity"]["per_rank"] == [-1] * n  # no golden at this size
+    assert out["e2e"]["parity"] is True and out["e2e"]["parity_per_rank"] == [1] * n
+    assert "error" not in out["e2e_inprocess"], out["e2e_inprocess"]
+    assert out["e2e_inprocess"]["parity"] is True and out["e2e_inprocess"]["parity_per_slice"] == [1] * n
+
+
+@pytest.mark.parametrize("n", [2, 8])
+def test_n_rank_line_carries_cpu_baseline_and_every_leg(n):
+    """bench.py's own main() in every rank (device calls on host stand-ins,
+    tests/bench_fake_rank.py), self-launched as the driver does at N GPUs."""
+    p = _run_spawner(n, script=FAKE, argv=["--gpus", str(n)] + FAKE_ARGV, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [x for x in p.stdout.splitlines() if x.strip()]
+    assert len(lines) == 1, p.stdout
+    out = json.loads(lines[0])
+    _check_line(out, n)
+    assert out["ranks"]["process_group"] == "gloo" and out["ranks"]["launcher"] == "bench.py"
+    assert "other_configs" not in out
+
+
+def test_one_rank_group_takes_the_n_rank_route():
+    """LBF_BENCH_FORM_GROUP=1 at --gpus 1 forms a one-rank group and runs the
+    N>1 flow (its -m gpu twin uses RCCL: tests/test_gpu_nccl.py)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    env.update(RANK="0", LOCAL_RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(bench._free_port()),
+               LBF_BENCH_FORM_GROUP="1", LBF_BENCH_BACKEND="gloo")
+    p = subprocess.run([sys.executable, FAKE, "--gpus", "1"] + FAKE_ARGV, env=env, capture_output=True, text=True,
+                       timeout=300, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    out = json.loads([x for x in p.stdout.splitlines() if x.strip()][-1])
+    _check_line(out, 1)
+    assert out["ranks"]["process_group"] == "gloo"
+
+
+def test_self_launch_refused_under_a_profiler():
+    """under rocprofv3 a self-launching bench.py would start GPU
+    children from a process the profiler's preload has initialised."""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    env["ROCPROF_OUTPUT_PATH"] = "/tmp/x"  # as rocprofv3 exports it (its preload is not loaded here)
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], env=env, capture_output=True,
+                       text=True, timeout=120, cwd=ROOT)
+    assert p.returncode != 0 and "not allowed under rocprofv3" in p.stderr, (p.returncode, p.stderr[-2000:])

@@ -3,7 +3,8 @@
 With one GPU the two ranks share it under gloo (a rehearsal); what is checked
 is the flow: two ranks, each rank's device-resident digests equal the oracle
 on its shard, and the N-rank host-memory legs (e2e, e2e_inprocess) report
-parity.  Small shards (256 MiB per rank) keep it to seconds."""
+parity, and rank 0's cpu_baseline is in the line.  Small shards (256 MiB per
+rank) keep it to seconds."""
 import hashlib
 import json
 import os
@@ -21,7 +22,7 @@ def test_bench_self_launched_two_ranks(oracle):
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
     env["LBF_BENCH_BACKEND"] = "gloo"
     args = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
-            "--file-gib", "0.25"]
+            "--file-gib", "0.25", "--cpu-min-s", "0.5"]
     p = subprocess.run(args, env=env, capture_output=True, text=True, timeout=240, cwd=ROOT)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = [x for x in p.stdout.splitlines() if x.strip()]
@@ -42,3 +43,6 @@ def test_bench_self_launched_two_ranks(oracle):
     inproc = out["e2e_inprocess"]
     assert "error" not in inproc, inproc
     assert inproc["parity"] is True and inproc["parity_per_slice"] == [1, 1] and inproc["bytes"] == 2 * per * cs
+    # the CPU comparator is in the N>1 line too, timed by rank 0 after the other rank finished
+    cb = out["cpu_baseline"]
+    assert cb["parity_vs_gpu"] is True and cb["value"] > 0 and "rank 0 alone" in cb["when"]
