@@ -1252,6 +1252,37 @@ struct Pin {
 std::mutex g_pin_mu;
 std::map<uintptr_t, Pin> g_pins;  // lo -> pin, disjoint ranges
 
+// The pinned host allocation that holds address p, as [base, end), if any.
+// hipMemGetAddressRange resolves host-pinned memory (hipHostMalloc,
+// hipHostRegister) by the host address or, failing that, by the device
+// address hipPointerGetAttributes reports for it.
+struct PinnedAlloc {
+  bool pinned = false;
+  uintptr_t base = 0, end = 0;  // end == 0: the extent is unknown
+};
+PinnedAlloc pinned_alloc(uintptr_t p) {
+  PinnedAlloc out;
+  hipPointerAttribute_t attr{};
+  out.pinned = hipPointerGetAttributes(&attr, reinterpret_cast<void*>(p)) == hipSuccess &&
+               attr.type == hipMemoryTypeHost;
+  (void)hipGetLastError();  // pageable memory is an error to that query
+  if (!out.pinned) return out;
+  const uintptr_t dev = reinterpret_cast<uintptr_t>(attr.devicePointer);
+  for (const uintptr_t q : {p, dev}) {
+    hipDeviceptr_t b = nullptr;
+    size_t size = 0;
+    const bool ok = q && hipMemGetAddressRange(&b, &size, reinterpret_cast<hipDeviceptr_t>(q)) == hipSuccess;
+    (void)hipGetLastError();
+    const uintptr_t bb = reinterpret_cast<uintptr_t>(b);
+    if (ok && size && bb <= q && q - bb < size) {
+      out.base = p - (q - bb);  // the same offset from the host base
+      out.end = out.base + size;
+      return out;
+    }
+  }
+  return out;
+}
+
 // Drop one reference to the pin at lo (pinned by this library).
 int unpin(uintptr_t lo) {
   std::lock_guard<std::mutex> lock(g_pin_mu);
@@ -1375,30 +1406,27 @@ extern "C" int lbf_host_register(lbf_ctx* ctx, const void* ptr, uint64_t len) {
     if (overlaps)
       return fail(LBF_ERR_INVALID, "lbf_host_register: range overlaps, but differs from, one another context holds");
     // Pinned already by someone else (a hipHostMalloc'd buffer, a caller's own
-    // registration): use it, never unpin it -- but only if the whole range is:
-    // both its first and its last page.  The first page alone may belong to a
-    // neighbouring pinned allocation.
-    auto pinned_page = [](uintptr_t p) {
-      hipPointerAttribute_t attr{};
-      const bool yes = hipPointerGetAttributes(&attr, reinterpret_cast<void*>(p)) == hipSuccess &&
-                       attr.type == hipMemoryTypeHost;
-      (void)hipGetLastError();  // pageable memory is an error to that query
-      return yes;
-    };
-    const bool first_pinned = pinned_page(r.lo), last_pinned = pinned_page(r.hi - page);
-    if (first_pinned && last_pinned) {
+    // registration): use it, never unpin it -- but only if ONE pinned
+    // allocation covers the whole range.  Its first and last page being pinned
+    // is not enough: they may belong to two neighbouring allocations with
+    // pageable memory between them, which a direct copy would then read.
+    const PinnedAlloc first = pinned_alloc(r.lo), last = pinned_alloc(r.hi - page);
+    if (first.pinned && first.base <= r.lo && r.hi <= first.end) {
       ctx->regs.push_back(r);
       return (int)LBF_OK;
     }
-    if (first_pinned || last_pinned)
+    if (first.pinned || last.pinned)
       return fail(LBF_ERR_INVALID,
-                  "lbf_host_register: range is partly pinned already (its first or last page belongs to another "
-                  "pinned allocation)");
+                  "lbf_host_register: range is partly pinned already (no single pinned allocation holds all of it)");
     KeepCurrentDevice keep;
     LBF_HIP_TRY(hipSetDevice(ctx->workers[0].device));
     const hipError_t e = hipHostRegister(reinterpret_cast<void*>(r.lo), r.hi - r.lo, hipHostRegisterPortable);
     if (e == hipErrorHostMemoryAlreadyRegistered) {
+      // pages inside the range are pinned by another allocation while its
+      // first and last are not (checked above): partly pinned
       (void)hipGetLastError();
+      return fail(LBF_ERR_INVALID, "lbf_host_register: range is partly pinned already (pages inside it belong to "
+                                   "another pinned allocation)");
     } else if (e != hipSuccess) {
       return hip_fail(e, "hipHostRegister");
     } else {

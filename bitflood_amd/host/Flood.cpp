@@ -149,14 +149,16 @@ Error::ErrorCode Flood::SetupFilesAndChunks() {
   for (const std::string& p : paths) cpaths.push_back(p.c_str());
   if (!offs.empty() && lbf_files_ranges(ctx, cpaths.data(), (U32)cpaths.size(), file_of.data(), offs.data(),
                                         sizes.data(), offs.size(), expected.data(), verdicts.data()) != LBF_OK) {
-    ret = Error::UNKNOWN_ERROR_LBF;
-    for (size_t f = 0; f < rtfs.size(); ++f) {  // one file at a time
+    // One file at a time; the call fails only if some file's own call fails
+    // too (a batch failure the retries recover from leaves complete state).
+    for (size_t f = 0; f < rtfs.size(); ++f) {
       const U64 b = first_of[f], e = first_of[f + 1];
       if (b == e) continue;
       const U32 zero = 0;
       V_U32 fo(e - b, zero);
       file_ok[f] = lbf_files_ranges(ctx, &cpaths[f], 1, fo.data(), offs.data() + b, sizes.data() + b, e - b,
                                     expected.data() + 20 * b, verdicts.data() + b) == LBF_OK;
+      if (!file_ok[f]) ret = Error::UNKNOWN_ERROR_LBF;
     }
   }
   for (size_t f = 0; f < rtfs.size(); ++f) {

@@ -249,6 +249,27 @@ int main(int argc, char** argv) {
       std::fwrite(bytes[1].data(), 1, bytes[1].size(), g);
       std::fclose(g);
     }
+    // the batched verify fails once (one-shot injected fault at the context's
+    // first group): each file is verified on its own, every retry succeeds, so
+    // Initialize reports success with complete chunkmaps
+    {
+      setenv("LBF_TEST_FAULT_GROUP", "0", 1);
+      lbf_ctx* fctx = nullptr;
+      const int made = lbf_ctx_create(1u, &fctx);
+      unsetenv("LBF_TEST_FAULT_GROUP");
+      CHECK(made == LBF_OK);
+      if (made == LBF_OK) {
+        FloodFileSPtr mff(new FloodFile(mf));
+        Flood mv3;
+        mv3.m_ctx = fctx;
+        CHECK(mv3.Initialize(mff) == Error::NO_ERROR_LBF);
+        CHECK(mv3.m_runtimefiles[files[0].first].m_chunkmap == "111");
+        CHECK(mv3.m_runtimefiles[files[1].first].m_chunkmap == "11");
+        CHECK(mv3.m_runtimefiles.size() == 3 && mv3.m_chunkstodownload.empty());
+        CHECK(mv3.m_totalbytes == files[0].second + files[1].second + files[2].second);
+        lbf_ctx_destroy(fctx);
+      }
+    }
     // a missing file: the call fails and the output is left as it was (:45-47, :96-99)
     me.m_files.push_back(dir + "/missing.bin");
     FloodFile untouched;

@@ -252,13 +252,15 @@ def test_device_ptr_batch(variant, hasher, oracle):
             b.free()
 
 
-def test_uniform_ragged_chain_count_between_16k_and_32k(variant, oracle):
-    """20,000 chains -- the automatic choice is pc4x2 there -- with a short last
-    chunk: the last workgroup's second group is partly idle (20,000 = 156 x 128
-    + 32).  Device-resident, every digest against the oracle."""
+@pytest.mark.parametrize("n", [20000, 20064])
+def test_uniform_ragged_chain_count_between_16k_and_32k(variant, oracle, n):
+    """Chain counts where the automatic choice is pc4x2, with a short last
+    chunk.  pc4x2 takes 128 chains per workgroup, two groups of 64.  At 20,000
+    = 156 x 128 + 32 the last workgroup's group 0 has 32 chains and group 1
+    none; at 20,064 = 156 x 128 + 96 group 0 is full and group 1 has 32
+    (ADVICE r03).  Device-resident, every digest against the oracle."""
     cs = 4096
-    n_bytes = 19999 * cs + 1000
-    n = 20000
+    n_bytes = (n - 1) * cs + 1000
     buf = DeviceBuffer(n_bytes)
     dig = DeviceBuffer(n * 20)
     try:

@@ -150,3 +150,70 @@ def test_failed_hip_call_does_not_fail_the_next_one(oracle, hasher):
     buf = oracle.synth(74, 0, 1 << 20, nthreads=4)
     offs, sizes = chunk_table(buf.size, 64 * 1024)
     assert np.array_equal(hasher.hash_chunks(buf, offs, sizes), oracle.sha1_batch(buf, offs, sizes, nthreads=4))
+
+
+def _hip():
+    """libamdhip64 (loaded by torch already) for pinning memory outside the library."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipHostMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_uint]
+    hip.hipHostFree.argtypes = [ctypes.c_void_p]
+    hip.hipHostRegister.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint]
+    hip.hipHostUnregister.argtypes = [ctypes.c_void_p]
+    return hip
+
+
+def test_memory_pinned_elsewhere_is_used_only_when_one_allocation_holds_it(oracle, hasher):
+    """a range whose first and last pages are pinned by two
+    different allocations, with pageable memory between them, used to pass the
+    'already pinned' check and go down the direct-copy route.  Now a range
+    pinned elsewhere is used as it is only when one pinned allocation covers
+    all of it; every other mix is refused."""
+    import ctypes
+    import mmap
+    hip = _hip()
+    # (1) a sub-range of one hipHostMalloc'd buffer: accepted, read directly, left pinned
+    p = ctypes.c_void_p()
+    assert hip.hipHostMalloc(ctypes.byref(p), 8 * MIB, 0) == 0
+    try:
+        whole = np.ctypeslib.as_array((ctypes.c_uint8 * (8 * MIB)).from_address(p.value))
+        whole[:] = oracle.synth(91, 0, 8 * MIB, nthreads=4)
+        sub = whole[MIB:5 * MIB]
+        offs, sizes = chunk_table(sub.size, 256 * 1024)
+        want = oracle.sha1_batch(sub, offs, sizes, nthreads=4)
+        hasher.register_host(sub)
+        s0 = hasher.staging_stats()
+        assert np.array_equal(hasher.hash_chunks(sub, offs, sizes), want)
+        assert _delta(hasher, s0)["direct"] == sub.size
+        hasher.unregister_host(sub)
+        assert np.array_equal(hasher.hash_chunks(sub, offs, sizes), want)  # still pinned, not ours to unpin
+    finally:
+        assert hip.hipHostFree(p) == 0
+    # (2) pinned | pageable | pinned: refused; the pageable middle alone is pinned by the library
+    mm = mmap.mmap(-1, 3 * MIB)
+    buf = np.frombuffer(mm, dtype=np.uint8)
+    base = buf.ctypes.data
+    assert hip.hipHostRegister(ctypes.c_void_p(base), MIB, 0) == 0
+    assert hip.hipHostRegister(ctypes.c_void_p(base + 2 * MIB), MIB, 0) == 0
+    try:
+        buf[:] = oracle.synth(92, 0, 3 * MIB, nthreads=4)
+        with pytest.raises(LbfError) as e:
+            hasher.register_host(buf)
+        assert e.value.status == _capi.LBF_ERR_INVALID and "partly pinned" in str(e.value)
+        # first page pinned, the rest pageable: refused too
+        with pytest.raises(LbfError) as e:
+            hasher.register_host(buf[:2 * MIB])
+        assert e.value.status == _capi.LBF_ERR_INVALID
+        mid = buf[MIB:2 * MIB]
+        hasher.register_host(mid)
+        offs, sizes = chunk_table(mid.size, 128 * 1024)
+        s0 = hasher.staging_stats()
+        assert np.array_equal(hasher.hash_chunks(mid, offs, sizes), oracle.sha1_batch(mid, offs, sizes))
+        assert _delta(hasher, s0)["direct"] == mid.size
+        hasher.unregister_host(mid)
+        # the whole buffer, unregistered, still hashes right through staging
+        offs, sizes = chunk_table(buf.size, 256 * 1024)
+        assert np.array_equal(hasher.hash_chunks(buf, offs, sizes), oracle.sha1_batch(buf, offs, sizes))
+    finally:
+        assert hip.hipHostUnregister(ctypes.c_void_p(base)) == 0
+        assert hip.hipHostUnregister(ctypes.c_void_p(base + 2 * MIB)) == 0

@@ -151,11 +151,37 @@ def test_c5_full_size_16gib(tmp_path):
     print("C5 16 GiB:", json.dumps({k: r[k] for k in ("seconds", "payload_gibs", "wire_gibs", "verify_latency_us",
                                                         "accept_latency_us", "leecher", "seeder", "encode_flood_s")}))
     assert r["chunks"] == 65536 and r["corrupted_sent"] == 65
-    # verify latency (frame arrival -> GPU verdict, before the disk write) at
-    # the default 10 ms batch deadline; 150 ms leaves room for
-    # slower hosts
+    # Latency at the default 10 ms batch deadline: verify =
+    # frame arrival -> GPU verdict (before the disk write), accept = arrival ->
+    # chunk written and marked.  Six fresh-box runs of round 3 measured verify
+    # p90 10.4-11.5 ms and p99 18-60 ms, accept p90 14-15.4 ms and p99 24-69 ms
+    # (profiles/r03/session{6,10,18,23,30,32}/pytest_gpu.txt).  The p90 bounds
+    # sit near 2x the measured p90, the p99 bounds above the worst p99; the
+    # session-3 tree (verify p99 252 ms, profiles/r03/suite_s3_failed_c5_p99.txt)
+    # fails both.
     assert r["deadline_ms"] == 10
-    assert r["verify_latency_us"]["p99"] < 150_000, r["verify_latency_us"]
+    v, a = r["verify_latency_us"], r["accept_latency_us"]
+    assert v["p90"] < 25_000 and v["p99"] < 100_000, v
+    assert a["p90"] < 30_000 and a["p99"] < 120_000, a
+
+
+@pytest.mark.gpu
+def test_per_chunk_base64encode_resume_loop_cost(tmp_path):
+    """The reference's resume verify unchanged (Flood.cpp:259-275: Base64Encode
+    once per chunk) over a 64 MiB file at 256 KiB chunks, against the batched
+    Flood::SetupFilesAndChunks and the same loop on one host core
+    (tests/c/per_chunk_resume.cpp).  All three must give the same chunkmap;
+    the times are printed for INTEGRATION.md (VERDICT r03 "Next round" #3)."""
+    exe = os.path.join(ROOT, "tests", "c", "build", "per_chunk_resume")
+    if not os.path.exists(exe):
+        subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "tests", "c")])
+    r = subprocess.run([exe, str(tmp_path), "64", "256"], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, (r.returncode, r.stdout, r.stderr[-2000:])
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    print("per-chunk resume loop:", json.dumps(out))
+    assert out["chunkmaps_equal"] is True and out["chunks"] == 256
+    # the batched call beats the per-chunk loop it replaces
+    assert out["batched_setup_files_and_chunks_s"] < out["per_chunk_base64encode_gpu_s"]
 
 
 def test_expected_xml_helper_matches_cpp_unit_case():
