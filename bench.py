@@ -294,7 +294,17 @@ def traffic_from_profiles(file_bytes, chunk_size, kernel):
         for e in d.get("entries", [d]):
             if (int(e.get("file_bytes", -1)) == int(file_bytes) and int(e.get("chunk_size", 262144)) == chunk_size
                     and kernel in e.get("kernel", "")):
-                return float(e["hbm_bytes_per_launch"]), e.get("source", p)
+                src = e.get("source", p)
+                b = e.get("bench_same_session")
+                if b and e.get("trace_timed_median_ns"):
+                    src += (f" (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE of this kernel at this size; recorded in one lease "
+                            f"with an unprofiled bench line of ms_per_step {b['ms_per_step']} and a kernel trace whose "
+                            f"timed dispatches have median {e['trace_timed_median_ns'] / 1e6:.4f} ms; a lookup, not "
+                            "this run's counters)")
+                else:
+                    src += (" (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, same kernel and size; a recorded lookup, not "
+                            "this run's counters)")
+                return float(e["hbm_bytes_per_launch"]), src
     except Exception:
         pass
     return None, None
@@ -843,8 +853,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "traffic_source": traffic_src and f"{traffic_src} (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, same "
-                                                  "kernel and size; a recorded lookup, not this run's counters)",
+                "traffic_source": traffic_src,
                 "kernel_ms": round(launch_s * 1e3, 4),
                 "algorithmic_bytes_per_launch": file_bytes,
                 # what the HBM fraction can reach at all: SHA-1 is a serial chain per
@@ -928,7 +937,8 @@ def main():
         if gpu0_numa is not None:
             cb["host"]["gpu0_numa_node"] = gpu0_numa
         cb["when"] = ("after the timed region and the host-memory legs, rank 0 alone"
-                      + (f" (ranks 1-{world - 1} have finished)" if world > 1 else ""))
+                      + ("" if world == 1 else " (rank 1 has finished)" if world == 2 else
+                         f" (ranks 1-{world - 1} have finished)"))
         out["cpu_baseline"] = cb
     if rank == 0:
         print(json.dumps(out), flush=True)

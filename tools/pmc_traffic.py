@@ -56,6 +56,23 @@ def main():
     os.makedirs(a.dst, exist_ok=True)
     out = {"file_bytes": a.file_bytes}
 
+    # the plain bench line of the same session (tools/profile_round.sh step 0):
+    # the evidence chain closes within one lease
+    try:
+        line = json.loads([x for x in open(os.path.join(a.src, "bench.json")) if x.startswith("{")][-1])
+        out["bench_same_session"] = {"value": line["value"], "ms_per_step": line["ms_per_step"],
+                                     "kernel_ms": line["roofline"]["kernel_ms"], "frac": line["roofline"]["frac"],
+                                     "kernel": line["config"]["kernel"]}
+    except (OSError, ValueError, KeyError, IndexError):
+        pass
+    # the bench line the traced run printed (its HIP events include the tracer's overhead)
+    try:
+        line = json.loads([x for x in open(os.path.join(a.src, "trace.log")) if x.startswith("{")][-1])
+        out["bench_traced_run"] = {"value": line["value"], "ms_per_step": line["ms_per_step"],
+                                   "kernel_ms": line["roofline"]["kernel_ms"], "steps": line["steps"],
+                                   "warmup": line["warmup"]}
+    except (OSError, ValueError, KeyError, IndexError):
+        pass
     stats = os.path.join(a.src, "trace", "trace_kernel_stats.csv")
     if os.path.exists(stats):
         shutil.copy(stats, os.path.join(a.dst, "kernel_stats.csv"))
@@ -69,6 +86,30 @@ def main():
                 out["kernel"] = r["Name"]
                 out["trace_avg_ns"] = float(r["AverageNs"])
                 out["trace_calls"] = int(r["Calls"])
+
+    # per-dispatch durations of the traced run: min / median beside the average
+    # (the average carries the warm-up launches and the tracer's own overhead)
+    trace = os.path.join(a.src, "trace", "trace_kernel_trace.csv")
+    if os.path.exists(trace) and "kernel" in out:
+        d = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in csv.DictReader(open(trace))
+             if r.get("Kernel_Name") == out["kernel"]]  # in dispatch order
+        # the timed steps are the traced bench's last `steps` dispatches of this kernel
+        steps = out.get("bench_traced_run", {}).get("steps", 0)
+        timed = sorted(d[-steps:]) if steps and len(d) >= steps else []
+        d = sorted(d)
+        if timed:
+            out["trace_timed_dispatches"] = len(timed)
+            out["trace_timed_median_ns"] = (timed[len(timed) // 2] if len(timed) % 2 else
+                                            (timed[len(timed) // 2 - 1] + timed[len(timed) // 2]) / 2)
+            out["trace_timed_mean_ns"] = sum(timed) / len(timed)
+        if d:
+            out["trace_dispatches"] = len(d)
+            out["trace_min_ns"] = d[0]
+            out["trace_median_ns"] = d[len(d) // 2] if len(d) % 2 else (d[len(d) // 2 - 1] + d[len(d) // 2]) / 2
+            out["trace_max_ns"] = d[-1]
+    for key in ("bench_same_session", "bench_traced_run"):
+        if key in out and "trace_median_ns" in out:
+            out[f"trace_median_over_{key}_ms_per_step"] = out["trace_median_ns"] / 1e6 / out[key]["ms_per_step"]
 
     def pick(sub):
         p = os.path.join(a.src, sub, "pmc_counter_collection.csv")
@@ -114,6 +155,9 @@ def main():
                "hbm_bytes_per_launch": out["hbm_bytes_per_launch"],
                "source": os.path.relpath(os.path.join(a.dst, "summary.json"), root),
                "kernel": out.get("kernel")}
+        for k in ("trace_median_ns", "trace_timed_median_ns", "bench_same_session", "bench_traced_run"):
+            if k in out:
+                rec[k] = out[k]
         try:
             old = json.load(open(path))
             entries = old.get("entries", [old])
