@@ -51,6 +51,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -79,6 +80,8 @@ struct Opts {
   bool keep = false;
   bool synthetic = false;
   bool register_arenas = true;  // --no-register: stage the leecher's verifies (A/B)
+  unsigned verifiers = 2;        // leecher: GPU verifies in flight (each its own context)
+  bool seeder_pipeline = false;  // --pipelined-seeder: verify batch k+1 while batch k is encoded
 };
 
 [[noreturn]] void die(const std::string& m) {
@@ -340,6 +343,10 @@ struct Chan {
 
 // Seeder pipeline: reader thread (frames -> request keys), this thread (read +
 // GPU verify + parallel encode of a batch), sender thread (frames -> socket).
+// --pipelined-seeder moves the encode to a thread of its own, so batch k+1 is
+// read and verified while batch k is encoded.  On the 16-CPU GPU box that did
+// not raise the transfer rate and cost latency: the generator and the encoder
+// then compete for the same cores, so it is not the default.
 void seeder_main(int lfd, FloodFileSPtr ff, std::string root, const Opts& o, SeederStats& st) {
   const int fd = accept(lfd, nullptr, nullptr);
   if (fd < 0) die("accept failed");
@@ -369,62 +376,44 @@ void seeder_main(int lfd, FloodFileSPtr ff, std::string root, const Opts& o, See
     while (outbox.take(msgs, 64))
       for (const std::string& m : msgs) ok = ok && send_all(fd, m);
   });
-  std::vector<Flood::P_ChunkKey> keys;
-  Flood::S_ChunkKey corrupted;
-  // One arena for the whole transfer, page-aligned and (unless --no-register)
-  // registered with the seeder's context, like the leecher's: a batch costs no
-  // allocation, no zero fill of up to batch x chunk bytes, and no staging copy
-  // on its verify.  ReadVerifiedChunks keeps its own vector the same way.
+  // Two arenas for the whole transfer (one being verified, one being encoded),
+  // page-aligned and (unless --no-register) registered with the seeder's
+  // context, like the leecher's: a batch costs no allocation, no zero fill of up
+  // to batch x chunk bytes, and no staging copy on its verify.
+  // ReadVerifiedChunks keeps its own vectors the same way.
+  constexpr int kSeedArenas = 2;
   const U64 page = (U64)sysconf(_SC_PAGESIZE);
   const U64 slot_bytes = ((U64)o.chunksize + 15) & ~15ull;
   const U64 synth_cap = (slot_bytes * o.batch + page - 1) / page * page;
-  U8* synth_arena = nullptr;
+  U8* synth_mem = nullptr;
   if (o.synthetic) {
-    synth_arena = static_cast<U8*>(aligned_alloc(page, synth_cap));
-    if (!synth_arena) die("seeder: cannot allocate the arena");
-    memset(synth_arena, 0, synth_cap);
-    if (o.register_arenas && lbf_host_register(ctx, synth_arena, synth_cap) != LBF_OK)
-      die("seeder: lbf_host_register failed: " + std::string(lbf_last_error()));
+    synth_mem = static_cast<U8*>(aligned_alloc(page, synth_cap * kSeedArenas));
+    if (!synth_mem) die("seeder: cannot allocate the arenas");
+    memset(synth_mem, 0, synth_cap * kSeedArenas);
+    for (int a = 0; a < kSeedArenas; ++a)
+      if (o.register_arenas && lbf_host_register(ctx, synth_mem + a * synth_cap, synth_cap) != LBF_OK)
+        die("seeder: lbf_host_register failed: " + std::string(lbf_last_error()));
   }
-  V_U8 file_arena;
-  while (requests.take(keys, o.batch)) {
-    st.requests += keys.size();
+  V_U8 file_arena[kSeedArenas];
+  struct Verified {
+    std::vector<Flood::P_ChunkKey> keys;
     V_U64 offs;
     std::string valid;
-    auto t0 = Clock::now();
-    if (o.synthetic) {
-      // the requested chunks from the generator, 16-byte aligned in the arena,
-      // then the same GPU re-verify before sending (ChunkMethods.cpp:116-123)
-      std::vector<Flood::ChunkArrival> chunks(keys.size());
-      offs.assign(keys.size(), 0);
-      U64 total = 0;
-      for (size_t k = 0; k < keys.size(); ++k) {
-        auto it = fl.m_runtimefiles.find(keys[k].first);
-        U32 sz = 0;
-        if (it != fl.m_runtimefiles.end() && keys[k].second < it->second.m_file->m_chunks.size())
-          sz = it->second.m_file->m_chunks[keys[k].second].m_size;
-        offs[k] = total;
-        chunks[k] = Flood::ChunkArrival{keys[k].first, keys[k].second, total, sz};
-        total += (sz + 15) & ~15ull;
-      }
-      if (total > synth_cap) die("seeder: batch larger than its arena");
-      parallel_for(keys.size(), o.threads, [&](size_t k) {
-        auto it = fl.m_runtimefiles.find(keys[k].first);
-        if (chunks[k].m_size == 0 || it == fl.m_runtimefiles.end()) return;
-        synth_bytes(synth_arena + offs[k], it->second.m_chunkoffsets[keys[k].second], chunks[k].m_size);
-      });
-      if (fl.VerifyChunks(synth_arena, synth_cap, chunks, valid) != Error::NO_ERROR_LBF)
-        die("seeder: verify failed: " + std::string(Encoder::LastError()));
-    } else if (fl.ReadVerifiedChunks(keys, file_arena, offs, valid) != Error::NO_ERROR_LBF) {
-      die("seeder: verify failed: " + std::string(Encoder::LastError()));
-    }
-    const U8* arena = o.synthetic ? synth_arena : file_arena.data();
+    int arena = 0;
+  };
+  Chan<Verified> to_encode;
+  Chan<int> free_arena;
+  for (int a = 0; a < kSeedArenas; ++a) free_arena.put(a);
+  Flood::S_ChunkKey corrupted;  // the encode stage's alone
+  auto encode = [&](Verified& v) {
+    const std::vector<Flood::P_ChunkKey>& keys = v.keys;
+    const U8* arena = o.synthetic ? synth_mem + v.arena * synth_cap : file_arena[v.arena].data();
     auto t1 = Clock::now();
     // sizes and the (first-send-only) corruption decision, serially
     std::vector<U32> sizes(keys.size(), 0);
     std::vector<char> flip(keys.size(), 0);
     for (size_t k = 0; k < keys.size(); ++k) {
-      if (valid[k] != '1') continue;
+      if (v.valid[k] != '1') continue;
       sizes[k] = fl.m_runtimefiles.find(keys[k].first)->second.m_file->m_chunks[keys[k].second].m_size;
       if (o.corrupt && sizes[k] && keys[k].second % o.corrupt == o.corrupt - 1 && corrupted.insert(keys[k]).second) {
         flip[k] = 1;
@@ -433,8 +422,8 @@ void seeder_main(int lfd, FloodFileSPtr ff, std::string root, const Opts& o, See
     }
     std::vector<std::string> out(keys.size());
     parallel_for(keys.size(), o.threads, [&](size_t k) {
-      if (valid[k] != '1') return;  // "send only if equal" (ChunkMethods.cpp:117-123)
-      const U8* data = arena + offs[k];
+      if (v.valid[k] != '1') return;  // "send only if equal" (ChunkMethods.cpp:117-123)
+      const U8* data = arena + v.offs[k];
       std::vector<U8> tmp;
       if (flip[k]) {  // a wire error after the seeder's own verify
         tmp.assign(data, data + sizes[k]);
@@ -443,9 +432,7 @@ void seeder_main(int lfd, FloodFileSPtr ff, std::string root, const Opts& o, See
       }
       out[k] = PeerWire::EncodeSendChunk(keys[k].first, keys[k].second, data, sizes[k]);
     });
-    auto t2 = Clock::now();
-    st.verify_s += secs(t0, t1);
-    st.encode_s += secs(t1, t2);
+    st.encode_s += secs(t1, Clock::now());
     for (std::string& m : out) {
       if (m.empty()) {
         ++st.refused;
@@ -454,14 +441,71 @@ void seeder_main(int lfd, FloodFileSPtr ff, std::string root, const Opts& o, See
       ++st.sent;
       outbox.put(std::move(m));
     }
+  };
+  std::thread encoder;
+  if (o.seeder_pipeline)
+    encoder = std::thread([&] {
+      std::vector<Verified> vs;
+      while (to_encode.take(vs, 1)) {
+        encode(vs[0]);
+        free_arena.put(vs[0].arena);
+      }
+    });
+  std::vector<Flood::P_ChunkKey> keys;
+  std::vector<int> ar;
+  while (requests.take(keys, o.batch)) {
+    st.requests += keys.size();
+    if (!free_arena.take(ar, 1)) break;
+    Verified v;
+    v.arena = ar[0];
+    auto t0 = Clock::now();
+    if (o.synthetic) {
+      // the requested chunks from the generator, 16-byte aligned in the arena,
+      // then the same GPU re-verify before sending (ChunkMethods.cpp:116-123)
+      U8* arena = synth_mem + v.arena * synth_cap;
+      std::vector<Flood::ChunkArrival> chunks(keys.size());
+      v.offs.assign(keys.size(), 0);
+      U64 total = 0;
+      for (size_t k = 0; k < keys.size(); ++k) {
+        auto it = fl.m_runtimefiles.find(keys[k].first);
+        U32 sz = 0;
+        if (it != fl.m_runtimefiles.end() && keys[k].second < it->second.m_file->m_chunks.size())
+          sz = it->second.m_file->m_chunks[keys[k].second].m_size;
+        v.offs[k] = total;
+        chunks[k] = Flood::ChunkArrival{keys[k].first, keys[k].second, total, sz};
+        total += (sz + 15) & ~15ull;
+      }
+      if (total > synth_cap) die("seeder: batch larger than its arena");
+      parallel_for(keys.size(), o.threads, [&](size_t k) {
+        auto it = fl.m_runtimefiles.find(keys[k].first);
+        if (chunks[k].m_size == 0 || it == fl.m_runtimefiles.end()) return;
+        synth_bytes(arena + v.offs[k], it->second.m_chunkoffsets[keys[k].second], chunks[k].m_size);
+      });
+      if (fl.VerifyChunks(arena, synth_cap, chunks, v.valid) != Error::NO_ERROR_LBF)
+        die("seeder: verify failed: " + std::string(Encoder::LastError()));
+    } else if (fl.ReadVerifiedChunks(keys, file_arena[v.arena], v.offs, v.valid) != Error::NO_ERROR_LBF) {
+      die("seeder: verify failed: " + std::string(Encoder::LastError()));
+    }
+    st.verify_s += secs(t0, Clock::now());
+    v.keys = std::move(keys);
+    keys = std::vector<Flood::P_ChunkKey>();
+    if (o.seeder_pipeline) {
+      to_encode.put(std::move(v));
+    } else {
+      encode(v);
+      free_arena.put(v.arena);
+    }
   }
+  to_encode.close();
+  if (encoder.joinable()) encoder.join();
   outbox.close();
   sender.join();
   reader.join();
   close(fd);
-  if (synth_arena) {
-    if (o.register_arenas) (void)lbf_host_unregister(ctx, synth_arena);
-    free(synth_arena);
+  if (synth_mem) {
+    for (int a = 0; a < kSeedArenas; ++a)
+      if (o.register_arenas) (void)lbf_host_unregister(ctx, synth_mem + a * synth_cap);
+    free(synth_mem);
   }
   lbf_ctx_destroy(ctx);
 }
@@ -494,15 +538,19 @@ int main(int argc, char** argv) {
     else if (a == "--keep") o.keep = true;
     else if (a == "--synthetic") o.synthetic = true;
     else if (a == "--no-register") o.register_arenas = false;
+    else if (a == "--verifiers") o.verifiers = (unsigned)strtoul(val(), nullptr, 10);
+    else if (a == "--pipelined-seeder") o.seeder_pipeline = true;
     else {
       fprintf(stderr,
               "usage: lbf_loopback [--size BYTES] [--chunksize N] [--window W] [--batch B] [--deadline-ms MS]\n"
               "                    [--threads T]\n"
-              "                    [--corrupt K] [--dir DIR] [--keep] [--synthetic] [--no-register]\n");
+              "                    [--corrupt K] [--dir DIR] [--keep] [--synthetic] [--no-register]\n"
+              "                    [--verifiers V] [--pipelined-seeder]\n");
       return 2;
     }
   }
   if (o.chunksize == 0 || o.window == 0 || o.batch == 0) die("chunksize, window and batch must be > 0");
+  if (o.verifiers == 0 || o.verifiers > 8) die("verifiers must be 1..8");
   if (o.dir.empty()) {
     const char* t = getenv("TMPDIR");
     char tmpl[512];
@@ -558,7 +606,8 @@ int main(int argc, char** argv) {
   std::deque<Flood::P_ChunkKey> todo(fl.m_chunkstodownload.begin(), fl.m_chunkstodownload.end());
   const std::vector<Flood::P_ChunkKey> all_keys(todo.begin(), todo.end());
   const size_t total = todo.size();
-  constexpr int kArenas = 4;  // one filling, one in GPU verify, one queued for it, one being written
+  // arenas: one filling, one per verifier, one queued for them, one being written
+  const int kArenas = (int)o.verifiers + 3;
   const U64 slot = ((U64)o.chunksize + 15) & ~15ull;
   // The arenas live for the whole transfer: pinned once, each batch's verify
   // copies them straight to HBM instead of through the context's staging
@@ -577,20 +626,38 @@ int main(int argc, char** argv) {
   };
   std::vector<Arena> arenas;
   for (int a = 0; a < kArenas; ++a) arenas.push_back(Arena{arena_mem + a * arena_stride, arena_len});
-  lbf_ctx* const leech_ctx = Encoder::Context();
-  if (!leech_ctx) die("leecher: no GPU context: " + std::string(Encoder::LastError()));
+  // One GPU context per verifier, so their verifies run side by side instead of
+  // one after another (a context runs one call at a time), each with a copy of
+  // the flood's chunk table (VerifyChunks only reads it).  Verifier 0 uses the
+  // process-wide context, like the writer.
+  std::vector<lbf_ctx*> vctx(o.verifiers, nullptr);
+  vctx[0] = Encoder::Context();
+  if (!vctx[0]) die("leecher: no GPU context: " + std::string(Encoder::LastError()));
+  for (unsigned v = 1; v < o.verifiers; ++v)
+    if (lbf_ctx_create(0, &vctx[v]) != LBF_OK) die(std::string("leecher: lbf_ctx_create: ") + lbf_last_error());
+  std::vector<std::unique_ptr<Flood>> vfl;
+  for (unsigned v = 0; v < o.verifiers; ++v) {
+    vfl.emplace_back(new Flood());
+    vfl[v]->m_floodfile = fl.m_floodfile;
+    vfl[v]->m_runtimefiles = fl.m_runtimefiles;
+    vfl[v]->m_rootdir = fl.m_rootdir;
+    vfl[v]->m_ctx = vctx[v];
+  }
   if (o.register_arenas)
-    for (const Arena& a : arenas)
-      if (lbf_host_register(leech_ctx, a.data(), a.size()) != LBF_OK)
-        die("leecher: lbf_host_register failed: " + std::string(lbf_last_error()));
+    for (lbf_ctx* c : vctx)
+      for (const Arena& a : arenas)
+        if (lbf_host_register(c, a.data(), a.size()) != LBF_OK)
+          die("leecher: lbf_host_register failed: " + std::string(lbf_last_error()));
   const int fd = connect_loopback(port);
 
   // Leecher pipeline: reader thread (frames), this thread (decode into one of
-  // kArenas arenas, bookkeeping, requests), verifier thread (VerifyChunks: the
-  // GPU verify, the verdict), writer thread (WriteChunks: the accepted chunks
-  // to disk, chunkmap '1').  ReceiveChunks split in two, so a batch's verify
-  // overlaps the next batch's decode and the previous batch's writes, and a
-  // slow disk does not hold up verdicts.
+  // kArenas arenas, bookkeeping, requests), --verifiers verifier threads
+  // (VerifyChunks: the GPU verify, the verdict; each its own context), writer
+  // thread (WriteChunks: the accepted chunks to disk, chunkmap '1').
+  // ReceiveChunks split in two, so a batch's verify overlaps the next batch's
+  // decode and the previous batch's writes, and a slow disk does not hold up
+  // verdicts.  With two verifiers a batch never waits for another batch's
+  // verify to finish before its own starts.
   struct Batch {
     std::vector<Arrival> got;
     std::vector<Flood::ChunkArrival> arr;
@@ -610,20 +677,24 @@ int main(int argc, char** argv) {
     while (rd.next(f)) arrivals.put(Arrival{std::move(f), Clock::now()});
     arrivals.close();
   });
-  std::thread verifier([&] {
-    std::vector<Batch> bs;
-    while (to_verify.take(bs, 1)) {
-      Batch& b = bs[0];
-      auto v0 = Clock::now();
-      if (fl.VerifyChunks(arenas[b.arena].data(), arenas[b.arena].size(), b.arr, b.valid) != Error::NO_ERROR_LBF)
-        die("leecher: VerifyChunks failed: " + std::string(Encoder::LastError()));
-      b.verdict = Clock::now();
-      b.verify_s = secs(v0, b.verdict);
-      --in_gpu;
-      to_write.put(std::move(b));
-    }
-    to_write.close();
-  });
+  std::atomic<unsigned> verifiers_left{o.verifiers};
+  std::vector<std::thread> verifier;
+  for (unsigned v = 0; v < o.verifiers; ++v)
+    verifier.emplace_back([&, v] {
+      std::vector<Batch> bs;
+      while (to_verify.take(bs, 1)) {
+        Batch& b = bs[0];
+        auto v0 = Clock::now();
+        if (vfl[v]->VerifyChunks(arenas[b.arena].data(), arenas[b.arena].size(), b.arr, b.valid) !=
+            Error::NO_ERROR_LBF)
+          die("leecher: VerifyChunks failed: " + std::string(Encoder::LastError()));
+        b.verdict = Clock::now();
+        b.verify_s = secs(v0, b.verdict);
+        --in_gpu;
+        to_write.put(std::move(b));
+      }
+      if (--verifiers_left == 0) to_write.close();
+    });
   std::thread writer([&] {
     std::vector<Batch> bs;
     while (to_write.take(bs, 1)) {
@@ -714,19 +785,20 @@ int main(int argc, char** argv) {
       if (in_verify == 0) {
         if (!arrivals.cv.wait_for(g, std::chrono::seconds(120), ready)) die("leecher: no chunk arrived for 120 s");
       } else {
-        // Batches are in flight.  With the GPU idle (they are only being
-        // written), start at once.  With one verify running, start the next
-        // batch once it is full (batches grow to what arrives during one
-        // verify) or once its oldest arrival has waited deadline_ms, which
-        // bounds the latency that growth adds.  With a batch already queued
-        // behind that verify, only a full batch goes: a smaller one would wait
-        // for the GPU anyway, and would cost one more chain of verify time.
+        // Batches are in flight.  With a verifier idle, start at once.  With
+        // every verifier busy, start the next batch once it is full (batches
+        // grow to what arrives during one verify) or once its oldest arrival
+        // has waited deadline_ms, which bounds the latency that growth adds.
+        // With a batch already queued behind them, only a full batch goes: a
+        // smaller one would wait for a verifier anyway, and would cost one more
+        // chain of verify time.
         const size_t gq = in_gpu.load();
         const auto deadline = std::chrono::milliseconds(o.deadline_ms);
         auto due = [&] {
           if (arrivals.q.size() >= o.batch || arrivals.closed) return true;
           if (arrivals.q.empty()) return false;
-          return gq == 0 || (gq == 1 && o.deadline_ms > 0 && Clock::now() - arrivals.q.front().t >= deadline);
+          return gq < o.verifiers ||
+                 (gq == o.verifiers && o.deadline_ms > 0 && Clock::now() - arrivals.q.front().t >= deadline);
         };
         if (!arrivals.cv.wait_for(g, std::chrono::milliseconds(1), due)) continue;
       }
@@ -773,10 +845,13 @@ int main(int argc, char** argv) {
   }
   const auto t_end = Clock::now();
   to_verify.close();
-  verifier.join();
+  for (std::thread& t : verifier) t.join();
   writer.join();
   if (o.register_arenas)
-    for (const Arena& a : arenas) (void)lbf_host_unregister(leech_ctx, a.data());
+    for (lbf_ctx* c : vctx)
+      for (const Arena& a : arenas) (void)lbf_host_unregister(c, a.data());
+  vfl.clear();
+  for (unsigned v = 1; v < o.verifiers; ++v) lbf_ctx_destroy(vctx[v]);
   free(arena_mem);
   shutdown(fd, SHUT_RDWR);
   reader.join();
@@ -798,7 +873,8 @@ int main(int argc, char** argv) {
   auto pct = [&](double p) { return pct_of(lat_us, p); };
   const double wall = secs(t_start, t_end);
   printf("{\"config\": \"C5 loopback 2-peer\", \"bytes\": %llu, \"chunk_size\": %u, \"chunks\": %zu, "
-         "\"window\": %u, \"batch\": %u, \"deadline_ms\": %u, \"threads\": %u, \"seconds\": %.3f, \"payload_gibs\": %.3f, "
+         "\"window\": %u, \"batch\": %u, \"deadline_ms\": %u, \"verifiers\": %u, \"seeder_pipelined\": %s, "
+         "\"threads\": %u, \"seconds\": %.3f, \"payload_gibs\": %.3f, "
          "\"wire_gibs\": %.3f, \"encode_flood_s\": %.3f, "
          "\"leecher\": {\"batches\": %zu, \"mean_batch\": %.1f, \"decode_s\": %.3f, \"verify_s\": %.3f, "
          "\"write_s\": %.3f, "
@@ -807,7 +883,8 @@ int main(int argc, char** argv) {
          "\"accept_latency_us\": {\"p50\": %.0f, \"p90\": %.0f, \"p99\": %.0f, \"max\": %.0f}, "
          "\"resume_verify_complete\": %s, \"files_identical\": %s, \"corrupt_every\": %u, \"corrupted_sent\": %llu, "
          "\"seed_source\": \"%s\", \"arenas_registered\": %s}\n",
-         (unsigned long long)o.size, o.chunksize, total, o.window, o.batch, o.deadline_ms, o.threads, wall,
+         (unsigned long long)o.size, o.chunksize, total, o.window, o.batch, o.deadline_ms, o.verifiers,
+         o.seeder_pipeline ? "true" : "false", o.threads, wall,
          payload / wall / (1u << 30), wire_bytes / wall / (1u << 30), encode_s, batches,
          batches ? (double)(accepted + rejected) / batches : 0.0, decode_s, verify_s, write_s, rejected, undecodable,
          (unsigned long long)sst.requests, (unsigned long long)sst.sent, (unsigned long long)sst.refused, sst.verify_s,

@@ -83,9 +83,10 @@ def test_loopback_needs_gpu():
     assert out.returncode == 2 and "no CPU fallback" in out.stderr
 
 
-def _loopback(tmp_path, size, cs, window, batch, corrupt, synthetic=False, threads=None, timeout=600, register=True):
+def _loopback(tmp_path, size, cs, window, batch, corrupt, synthetic=False, threads=None, timeout=600, register=True,
+              extra=()):
     args = [os.path.join(LIB, "lbf_loopback"), "--size", str(size), "--chunksize", str(cs), "--window", str(window),
-            "--batch", str(batch), "--corrupt", str(corrupt), "--dir", str(tmp_path / "c5")]
+            "--batch", str(batch), "--corrupt", str(corrupt), "--dir", str(tmp_path / "c5")] + list(extra)
     if synthetic:
         args.append("--synthetic")
     if threads:
@@ -125,6 +126,22 @@ def test_loopback_two_peers(tmp_path, size, cs, window, batch, corrupt, syntheti
     equals the source (a file, or with --synthetic the generated stream) byte
     for byte."""
     _loopback(tmp_path, size, cs, window, batch, corrupt, synthetic)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("extra,synthetic", [
+    (["--verifiers", "1"], False),                        # round 3's shape: one verify in flight
+    (["--verifiers", "1", "--pipelined-seeder"], True),
+    (["--verifiers", "4"], True),                         # four leecher contexts verifying side by side
+    (["--verifiers", "3", "--pipelined-seeder"], False),
+])
+def test_loopback_verifier_counts(tmp_path, extra, synthetic):
+    """The leecher's verifiers (each with its own GPU context and a copy of the
+    chunk table) and the seeder's verify/encode stages: same end state for
+    every count -- the written file equals the source, every corrupted arrival
+    is rejected and fetched again."""
+    r = _loopback(tmp_path, (32 << 20) + 12345, 65536, 512, 128, 7, synthetic, extra=extra)
+    assert r["verifiers"] == int(extra[1]) and r["seeder_pipelined"] is ("--pipelined-seeder" in extra)
 
 
 @pytest.mark.gpu
