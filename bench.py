@@ -271,9 +271,9 @@ def backend_name():
 
 
 def under_profiler():
-    """A profiler's preloaded library (rocprofv3) is in this process."""
-    pre = os.environ.get("LD_PRELOAD", "")
-    return "rocprof" in pre or any(k.startswith("ROCPROF") for k in os.environ)
+    """rocprofv3's preloaded tool library is in this process (the preload is
+    what initialises the GPU before the program starts)."""
+    return "rocprof" in os.environ.get("LD_PRELOAD", "")
 
 
 def barrier(world):

@@ -166,7 +166,9 @@ def test_self_launch_refused_under_a_profiler():
     """under rocprofv3 a self-launching bench.py would start GPU
     children from a process the profiler's preload has initialised."""
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
-    env["ROCPROF_OUTPUT_PATH"] = "/tmp/x"  # as rocprofv3 exports it (its preload is not loaded here)
+    # rocprofv3's tool library as the preload names it (a path that does not
+    # exist here: the loader warns and goes on, and bench.py reads the variable)
+    env["LD_PRELOAD"] = (env.get("LD_PRELOAD", "") + " /nonexistent/librocprofiler-sdk-tool.so").strip()
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], env=env, capture_output=True,
                        text=True, timeout=120, cwd=ROOT)
     assert p.returncode != 0 and "not allowed under rocprofv3" in p.stderr, (p.returncode, p.stderr[-2000:])
