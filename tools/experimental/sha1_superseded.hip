@@ -22,6 +22,7 @@
 //              layout, scheduling fences, twelve-step loop, consumer priority)
 //   16, 20    pc4 with its fast loop unrolled by four / sixteen
 //   25-28     pc4x2 producer priorities (25 = the shipped variant 12's code)
+//   34-36     pc4x2 in an 8-wave workgroup, consumers the oldest waves (round 4)
 // (The pc4 producer-priority variants 29-33 of round 3 measured 0.1-0.5 %,
 // below the noise, and are not rebuilt.)
 #include <hip/hip_runtime.h>
@@ -595,6 +596,100 @@ __global__ void __launch_bounds__(192 * kGroups) sha1_pc4x2_diag_kernel(ChunkPar
 }
 
 // ---------------------------------------------------------------------------
+// pc4x2 in an 8-wave workgroup (variants 34-36, round 4): the consumers are
+// the OLDEST waves.  In pc4x2 the consumers must be waves 2 and 3 to own a SIMD
+// (waves k and k+4 share one), so they are younger than the producers of waves
+// 0 and 1, and the CU serves older waves first; wave priorities recovered most
+// of that.  Here the workgroup has 8 waves: 0 and 1 consume (groups 0 and 1),
+// 4 and 5 end at once (s_barrier waits only for the waves still running), so
+// each consumer has its SIMD to itself, and 2, 3 (group 0) and 6, 7 (group 1)
+// produce, two to a SIMD as in pc4x2.  Same LDS layout and step protocol.
+// kPrioC: consumers' wave priority; kPrioG1: group 1's producers' priority.
+// ---------------------------------------------------------------------------
+template <bool kUniform, int kPrioC, int kPrioG1>
+__global__ void __launch_bounds__(512) sha1_pc4x2w8_kernel(ChunkParams p) {
+  extern __shared__ __attribute__((aligned(16))) uint4 lds[];  // group 0 | group 1: W[3][20][64] | raw[2][2][4][64]
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (wave == 4 || wave == 5) return;  // their SIMDs belong to the consumers
+  const bool consumer = wave < 2;
+  const int g = consumer ? wave : (wave < 4 ? 0 : 1);
+  const uint32_t first = blockIdx.x * (2 * kPcLanes);
+  const uint32_t i = first + g * kPcLanes + lane;
+  const ChainInfo c = chain_info<kUniform>(p, i);
+  const uint32_t other = chain_info<kUniform>(p, first + (1 - g) * kPcLanes + lane).total;
+  const uint32_t nsteps = __builtin_amdgcn_readfirstlane(max(wave_max(c.total), wave_max(other)));
+  uint4* ring = lds + g * kPc4x2GroupU4;
+
+  if (!consumer) {
+    // ---------------- producer X of group g: steps X, X+2, ... ----------------
+    if (kPrioG1 != 0 && g == 1) __builtin_amdgcn_s_setprio(kPrioG1);
+    const uint32_t X = wave & 1;
+    uint4* raw = ring + kPc4x2Ring * kPcSlotU4 + X * (kP2Raw * kPcRawU4);
+    const uint32_t raw_lds = (uint32_t)reinterpret_cast<uintptr_t>(raw);
+    p2_dma(c, X, raw_lds, 0);
+    p2_dma(c, X + 2, raw_lds, 1);
+    uint32_t w[16];
+    auto first_half = [&](uint32_t step) {
+      const uint32_t j = (step - X) >> 1;
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // block j landed; only j+1's DMAs pending
+      p2_block(w, raw + (j & 1u) * kPcRawU4 + lane, c, step);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // raw slot read before it is refilled
+      p2_dma(c, step + 4, raw_lds, j & 1u);
+      pc4x2_store_half<0>(w, ring, step, lane);
+    };
+    if (nsteps > 0) {
+      if (X < nsteps) {
+        first_half(X);
+        pc4x2_store_half<1>(w, ring, X, lane);
+      }
+      __syncthreads();  // barrier E: steps 0 and 1 complete
+    }
+    for (uint32_t b = 0; b < nsteps; ++b) {
+      const uint32_t fin = b + 1;
+      if ((fin & 1u) == X && fin < nsteps && b > 0) pc4x2_store_half<1>(w, ring, fin, lane);
+      const uint32_t start = b + 2;
+      if ((start & 1u) == X && start < nsteps) first_half(start);
+      __syncthreads();  // barrier b: steps <= b + 1 complete
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA outlives the workgroup
+  } else {
+    // ---------------- consumer of group g ----------------
+    if (kPrioC != 0) __builtin_amdgcn_s_setprio(kPrioC);
+    Digest s;
+    s.init();
+    Pc4Sched<2> A, B;
+    const uint32_t min_steps = __builtin_amdgcn_readfirstlane(wave_min(i < p.n ? c.total : 0xFFFFFFFFu));
+    if (nsteps > 0) {
+      __syncthreads();  // barrier E
+      A.load_all(Pc4Sched<2>::col(ring, 0, lane));
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): slot 0 is free from barrier 0 on
+      pc4_barrier(s);  // barrier 0
+    }
+    uint32_t k = 0;
+    const uint32_t fast_end = __builtin_amdgcn_readfirstlane(nsteps ? min(min_steps, nsteps - 1) : 0u);
+    for (; k + 6 <= fast_end; k += 6) {
+#pragma unroll
+      for (int j = 0; j < 6; j += 2) {
+        pc4_step(s, A, B, Pc4Sched<2>::col(ring, (j + 1) % kPc4x2Ring, lane), true, true);
+        pc4_barrier(s);
+        pc4_step(s, B, A, Pc4Sched<2>::col(ring, (j + 2) % kPc4x2Ring, lane), true, true);
+        pc4_barrier(s);
+      }
+    }
+    for (; k < nsteps; k += 2) {
+      pc4_step(s, A, B, Pc4Sched<2>::col(ring, (k + 1) % kPc4x2Ring, lane), k < c.total, k < min_steps);
+      if (k + 1 >= nsteps) break;
+      pc4_barrier(s);
+      pc4_step(s, B, A, Pc4Sched<2>::col(ring, (k + 2) % kPc4x2Ring, lane), k + 1 < c.total, k + 1 < min_steps);
+      if (k + 2 >= nsteps) break;
+      pc4_barrier(s);
+    }
+    if (i < p.n) write_result(p, i, s);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // The launch table
 // ---------------------------------------------------------------------------
 using Kern = void (*)(ChunkParams);
@@ -645,6 +740,9 @@ const Entry kTable[] = {
      &sha1_pc4x2_diag_kernel<true, 2, true, 3, false, 6, true, 0, 2>, 128, 384, kPc4x2LdsBytes},
     {28, &sha1_pc4x2_diag_kernel<false, 2, true, 3, false, 6, true, 1, 2>,
      &sha1_pc4x2_diag_kernel<true, 2, true, 3, false, 6, true, 1, 2>, 128, 384, kPc4x2LdsBytes},
+    {34, &sha1_pc4x2w8_kernel<false, 3, 1>, &sha1_pc4x2w8_kernel<true, 3, 1>, 128, 512, kPc4x2LdsBytes},
+    {35, &sha1_pc4x2w8_kernel<false, 0, 0>, &sha1_pc4x2w8_kernel<true, 0, 0>, 128, 512, kPc4x2LdsBytes},
+    {36, &sha1_pc4x2w8_kernel<false, 0, 1>, &sha1_pc4x2w8_kernel<true, 0, 1>, 128, 512, kPc4x2LdsBytes},
 };
 
 const Entry* find_entry(int variant) {

@@ -37,19 +37,22 @@ def main():
     ap.add_argument("--points", default="", help="chunk_size:count,... instead of the built-in list")
     a = ap.parse_args()
     size = a.max_gib * GIB
-    buf = DeviceBuffer(size)
-    buf.fill_synthetic(0x5EED)
-    dig = DeviceBuffer((size // 65536 + 1) * 20)
-    H.synchronize()
-    lib = load()
     points = [(262144, n) for n in (4096, 8192, 16384, 32768, 65536, 131072, 262144)]
     points += [(1 << 20, n) for n in (8192, 16384, 32768, 65536)]
     points += [(65536, n) for n in (16384, 65536, 262144, 1048576)]
     if a.points:
         points = [tuple(int(x) for x in pt.split(":")) for pt in a.points.split(",")]
+    points = [(cs, n) for cs, n in points if n * cs <= size]
+    if not points:
+        return
+    buf = DeviceBuffer(size)
+    buf.fill_synthetic(0x5EED)
+    # digests for the largest chunk count swept (the kernels write n x 20 bytes)
+    dig = DeviceBuffer(max(n for _, n in points) * 20)
+    H.synchronize()
+    lib = load()
     for cs, n in points:
-        if n * cs > size:
-            continue
+        assert n * 20 <= dig.nbytes and n * cs <= buf.nbytes
         ref = None
         for v in [int(x) for x in a.variants.split(",")]:
             H.set_kernel_variant(v)
