@@ -180,6 +180,28 @@ int launch_chunks(const ChunkParams& p, hipStream_t stream) {
 
 using lbf::fail;
 
+// A device array the caller passed must fit in the allocation it points into:
+// a launch that would run past one (a digest array sized for fewer chunks than
+// the launch writes) is refused before the kernel runs, since an out-of-bounds
+// write is a GPU fault.  Memory HIP cannot place (an allocator it does not
+// track) is not checked; the chunk bytes of a table launch are not either (the
+// offsets are on the device).
+static int check_fits(const void* p, uint64_t bytes, const char* what) {
+  if (!p || bytes == 0) return LBF_OK;
+  hipDeviceptr_t base = nullptr;
+  size_t size = 0;
+  if (hipMemGetAddressRange(&base, &size, const_cast<void*>(p)) != hipSuccess) {
+    (void)hipGetLastError();
+    return LBF_OK;
+  }
+  const uintptr_t b = reinterpret_cast<uintptr_t>(base), q = reinterpret_cast<uintptr_t>(p);
+  if (q < b || q - b > size || bytes > size - (q - b))
+    return fail(LBF_ERR_INVALID, std::string(what) + ": " + std::to_string(bytes) + " bytes from this pointer run past " +
+                                     "its allocation (" + std::to_string(size - std::min<uintptr_t>(q - b, size)) +
+                                     " bytes left)");
+  return LBF_OK;
+}
+
 static int check_out_alignment(const uint8_t* d_digests, const uint8_t* d_expected) {
   if ((reinterpret_cast<uintptr_t>(d_digests) & 3u) || (reinterpret_cast<uintptr_t>(d_expected) & 3u))
     return fail(LBF_ERR_INVALID, "digest/expected arrays must be 4-byte aligned");
@@ -196,6 +218,11 @@ extern "C" int lbf_sha1_launch(const uint8_t* d_base, const uint64_t* d_offsets,
   if ((d_verdicts != nullptr) != (d_expected != nullptr))
     return fail(LBF_ERR_INVALID, "lbf_sha1_launch: expected and verdicts go together");
   if (int rc = check_out_alignment(d_digests, d_expected)) return rc;
+  if (int rc = check_fits(d_offsets, 8 * n, "lbf_sha1_launch: offsets")) return rc;
+  if (int rc = check_fits(d_sizes, 4 * n, "lbf_sha1_launch: sizes")) return rc;
+  if (int rc = check_fits(d_digests, 20 * n, "lbf_sha1_launch: digests")) return rc;
+  if (int rc = check_fits(d_expected, 20 * n, "lbf_sha1_launch: expected")) return rc;
+  if (int rc = check_fits(d_verdicts, n, "lbf_sha1_launch: verdicts")) return rc;
   lbf::ChunkParams p{};
   p.base = d_base;
   p.offsets = d_offsets;
@@ -220,6 +247,10 @@ extern "C" int lbf_sha1_uniform_launch(const uint8_t* d_base, uint64_t len, uint
   if ((d_verdicts != nullptr) != (d_expected != nullptr))
     return fail(LBF_ERR_INVALID, "lbf_sha1_uniform_launch: expected and verdicts go together");
   if (int rc = check_out_alignment(d_digests, d_expected)) return rc;
+  if (int rc = check_fits(d_base, len, "lbf_sha1_uniform_launch: region")) return rc;
+  if (int rc = check_fits(d_digests, 20 * n, "lbf_sha1_uniform_launch: digests")) return rc;
+  if (int rc = check_fits(d_expected, 20 * n, "lbf_sha1_uniform_launch: expected")) return rc;
+  if (int rc = check_fits(d_verdicts, n, "lbf_sha1_uniform_launch: verdicts")) return rc;
   lbf::ChunkParams p{};
   p.base = d_base;
   p.len = len;
@@ -248,6 +279,7 @@ extern "C" int lbf_fill_synthetic(uint8_t* d_buf, uint64_t len, uint64_t seed, u
   if (len == 0) return LBF_OK;
   if (!d_buf || (start & 7u) || (reinterpret_cast<uintptr_t>(d_buf) & 15u))
     return fail(LBF_ERR_INVALID, "lbf_fill_synthetic: need start%8==0 and a 16-byte aligned buffer");
+  if (int rc = check_fits(d_buf, len, "lbf_fill_synthetic")) return rc;
   const uint64_t pairs = ((len >> 3) + 1) >> 1;
   uint64_t blocks = (pairs + 255) / 256;
   if (blocks > 8192) blocks = 8192;

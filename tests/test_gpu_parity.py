@@ -489,3 +489,34 @@ def test_hash_and_verify_many_files_one_batch(hasher, oracle, tmp_path):
     assert np.array_equal(v, exp_v)
     with pytest.raises(Exception):
         hasher.hash_files(paths, file_of, offs, sizes)  # a missing file fails hash mode
+
+
+def test_launch_refuses_device_arrays_too_small(hasher, oracle):
+    """A device array the caller passes must fit its allocation: a launch that
+    would write past a digest / verdict array (or read past the region or the
+    chunk table) is refused before any kernel runs, since an out-of-bounds
+    write is a GPU fault.  Arrays of exactly the right size are accepted."""
+    from bitflood_amd import LbfError
+    from bitflood_amd import _capi
+    cs, n = 4096, 100
+    buf, dig, small = DeviceBuffer(n * cs), DeviceBuffer(n * 20), DeviceBuffer(20 * 10)
+    offs, sizes = DeviceBuffer(8 * n), DeviceBuffer(4 * (n - 1))
+    try:
+        buf.fill_synthetic(93)
+        for call, what in [
+                (lambda: H.uniform_launch(buf, n * cs, cs, 0, n, small), "digests"),
+                (lambda: H.uniform_launch(buf.ptr + cs, n * cs, cs, 0, n, dig), "region"),
+                (lambda: H.batch_launch(buf, offs, sizes, n, dig), "sizes"),
+                (lambda: _capi.check(_capi.load().lbf_fill_synthetic(buf.ptr + 16, n * cs, 1, 0, None)),
+                 "lbf_fill_synthetic")]:
+            with pytest.raises(LbfError) as e:
+                call()
+            assert e.value.status == _capi.LBF_ERR_INVALID and what in str(e.value), str(e.value)
+        # exact sizes pass, and the digests are right
+        H.uniform_launch(buf, n * cs, cs, 0, n, dig)
+        H.synchronize()
+        want = oracle.encode_buffer(oracle.synth(93, 0, n * cs), cs)
+        assert np.array_equal(dig.download(n * 20).reshape(n, 20), want)
+    finally:
+        for b in (buf, dig, small, offs, sizes):
+            b.free()
