@@ -862,6 +862,11 @@ def main():
                 "ceiling_frac": round(file_bytes / (floor_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                 "ceiling_reason": (f"{n_chunks} serial SHA-1 chains: the issue floor below ({floor_ms:.3f} ms) "
                                    "bounds the launch, not HBM"),
+                "per": "GPU (the slowest rank's HIP-event launch time)",
+                # all N GPUs together: N shards in the slowest rank's launch time,
+                # against N x the HBM peak
+                "aggregate_achieved": round(world * achieved_gbs, 2),
+                "aggregate_peak": world * HBM_PEAK_GBS,
             },
             # SHA-1 is integer VALU work on a serial chain per chunk: the binding
             # limit is instruction issue, not HBM.

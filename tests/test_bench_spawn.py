@@ -124,6 +124,7 @@ def _check_line(out, n):
     assert out["n_gpus"] == n and out["scaling"] == "weak" and out["value"] > 0
     r = out["roofline"]
     assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 8000.0 and r["achieved"] > 0
+    assert r["aggregate_peak"] == n * 8000.0 and abs(r["aggregate_achieved"] - n * r["achieved"]) <= 0.01 * n
     cb = out["cpu_baseline"]
     assert cb["kind"] == "port" and cb["unit"] == "GiB/s" and cb["value"] > 0 and cb["cores"] >= 1
     assert cb["parity_vs_gpu"] is True and cb["host"]["usable_cores"] >= 1
