@@ -1,0 +1,211 @@
+// kern_b64.hpp -- the receiver's base64 decode on the device (gfx950).
+//
+// A SendChunk frame carries the chunk as XML-RPC base64 text
+// (/root/reference/cpp/src/ChunkMethods.cpp:141-163, decoded by xmlrpc++ 0.7
+// XmlRpcValue::binaryFromXml, XmlRpcValue.cpp:417-436, with the decoder of
+// base64.h:215-330).  lbf_b64_verify_batch decodes each chunk's text here, in
+// HBM, and the shipped hash kernels verify the decoded bytes where they lie,
+// so the receiver's two per-chunk passes (decode, then hash) both run on the
+// GPU and only the text crosses PCIe on the way in.
+//
+// Decode rules (base64.h:215-330, restated in bitflood_amd/host/PeerWire.cpp
+// Base64Get and tests/test_gpu_b64.py):
+//   - characters outside the alphabet (the frame's spaces, anything else) are
+//     skipped;
+//   - the remaining characters S[0..m) are taken four at a time; a group that
+//     holds '=' ends the data: "xx==" gives one byte, "xxx=" two, '=' in the
+//     first or second place none; an incomplete last group gives nothing.
+// So with q = the index of the first '=' in S (m if none), the output is the
+// 3 * floor(min(q, m) / 4) bytes of the complete groups, plus one byte when
+// q % 4 == 2 or two when q % 4 == 3 (q < m).
+//
+// One workgroup per chunk.  Pass 1 compacts the text: 4 KiB tiles, each lane
+// classifies 16 characters, a workgroup scan gives every valid character its
+// index in S, and the sextets are written to a scratch area laid out like the
+// text.  Pass 2 turns four groups (16 sextets, one 16-byte load) into 12 bytes
+// per lane.  Both passes stream: the bound is HBM (about 4.1 bytes moved per
+// decoded byte: text read, sextets written and read, bytes written).
+//
+// Part of the single translation unit sha1_kernels.hip (included from there).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "lbf_internal.hpp"
+
+namespace lbf {
+namespace {
+
+constexpr uint8_t kB64Eq = 64, kB64Skip = 255;
+constexpr int kB64Threads = 256;  // one lane per entry of the decode table below
+
+struct B64Table {
+  uint8_t v[256];
+};
+
+constexpr B64Table make_b64_table() {
+  B64Table t{};
+  for (int c = 0; c < 256; ++c) t.v[c] = kB64Skip;
+  for (int c = 'A'; c <= 'Z'; ++c) t.v[c] = (uint8_t)(c - 'A');
+  for (int c = 'a'; c <= 'z'; ++c) t.v[c] = (uint8_t)(26 + c - 'a');
+  for (int c = '0'; c <= '9'; ++c) t.v[c] = (uint8_t)(52 + c - '0');
+  t.v['+'] = 62;
+  t.v['/'] = 63;
+  t.v['='] = kB64Eq;
+  return t;
+}
+
+__constant__ B64Table g_b64_table = make_b64_table();
+
+// Exclusive scan of one value per lane over the 256-lane workgroup; returns
+// the lane's prefix and writes the total to *total.  `sums` is 4 words of LDS.
+__device__ __forceinline__ uint32_t wg_exclusive_scan(uint32_t v, uint32_t* sums, uint32_t* total) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)x, off, 64);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) sums[wave] = x;
+  __syncthreads();
+  uint32_t before = 0, all = 0;
+#pragma unroll
+  for (int w = 0; w < kB64Threads / 64; ++w) {
+    const uint32_t s = sums[w];
+    before += w < wave ? s : 0u;
+    all += s;
+  }
+  __syncthreads();  // sums is reused by the next call
+  *total = all;
+  return before + x - v;
+}
+
+// blockIdx.x = chunk.  Chunk i's text is text[text_off[i] .. + text_len[i])
+// (any alignment; 4-byte aligned reads faster) and its sextets go to
+// scratch[sext_off[i] ..) (16-byte aligned, room for text_len[i]: the
+// compacted stream is never longer than the text).  out[out_off[i] .. + cap[i])
+// receives the decoded bytes; sizes[i] = min(decoded length, cap[i]) and
+// over[i] = 1 when the text decodes to more than cap[i] bytes.
+__global__ void __launch_bounds__(kB64Threads) b64_decode_kernel(const uint8_t* __restrict__ text,
+                                                                 uint8_t* __restrict__ scratch,
+                                                                 const uint64_t* __restrict__ text_off,
+                                                                 const uint64_t* __restrict__ sext_off,
+                                                                 const uint32_t* __restrict__ text_len,
+                                                                 uint8_t* __restrict__ out,
+                                                                 const uint64_t* __restrict__ out_off,
+                                                                 const uint32_t* __restrict__ cap,
+                                                                 uint32_t* __restrict__ sizes,
+                                                                 uint8_t* __restrict__ over) {
+  __shared__ uint32_t sums[kB64Threads / 64];
+  __shared__ uint32_t first_eq;
+  __shared__ uint8_t tab[256];  // per-lane lookups: LDS serves divergent addresses, the constant table does not
+  tab[threadIdx.x] = g_b64_table.v[threadIdx.x];
+  const uint32_t i = blockIdx.x;
+  const uint8_t* t = text + text_off[i];
+  uint8_t* s = scratch + sext_off[i];
+  const uint32_t len = text_len[i];
+  if (threadIdx.x == 0) first_eq = 0xFFFFFFFFu;
+  __syncthreads();
+  // ---- pass 1: compact the alphabet characters (and '=') into sextets ----
+  uint32_t base = 0;  // sextets written by earlier tiles
+  for (uint32_t tile = 0; tile < len; tile += kB64Threads * 16) {
+    const uint32_t at = tile + threadIdx.x * 16;
+    uint8_t c[16];
+    if (at + 16 <= len) {
+      // the text of a chunk need not be 16-byte aligned: four dword loads
+      // when it is 4-byte aligned, bytes otherwise
+      if ((reinterpret_cast<uintptr_t>(t + at) & 3u) == 0) {
+        const uint32_t* p = reinterpret_cast<const uint32_t*>(t + at);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t w = p[k];
+          c[4 * k] = (uint8_t)w;
+          c[4 * k + 1] = (uint8_t)(w >> 8);
+          c[4 * k + 2] = (uint8_t)(w >> 16);
+          c[4 * k + 3] = (uint8_t)(w >> 24);
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) c[k] = t[at + k];
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 16; ++k) c[k] = at + k < len ? t[at + k] : (uint8_t)' ';
+    }
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      c[k] = tab[c[k]];
+      cnt += c[k] != kB64Skip;
+    }
+    uint32_t total;
+    uint32_t pos = base + wg_exclusive_scan(cnt, sums, &total);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      if (c[k] == kB64Skip) continue;
+      if (c[k] == kB64Eq) atomicMin(&first_eq, pos);
+      s[pos++] = c[k];
+    }
+    base += total;
+  }
+  __threadfence_block();
+  __syncthreads();
+  const uint32_t m = base, q = min(first_eq, m);
+  const uint32_t groups = q / 4;  // complete groups before any '='
+  const uint32_t r = q % 4;
+  // q < m: S[q] is '=': "xx=" gives one byte, "xxx=" two.  q == m: an
+  // incomplete last group gives nothing.
+  const uint32_t extra = q < m ? (r == 2 ? 1u : r == 3 ? 2u : 0u) : 0u;
+  const uint64_t want = 3ull * groups + extra;
+  const uint32_t limit = cap[i];
+  uint8_t* o = out + out_off[i];
+  // ---- pass 2: four groups (16 sextets) -> 12 bytes per lane ----
+  for (uint32_t g4 = threadIdx.x * 4; g4 < groups; g4 += kB64Threads * 4) {
+    uint8_t v[16];
+    if (g4 + 4 <= groups) {
+      const uint4 w = *reinterpret_cast<const uint4*>(s + 4ull * g4);  // 16-byte aligned: s is
+      const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+      for (int k = 0; k < 16; ++k) v[k] = (uint8_t)(ws[k >> 2] >> (8 * (k & 3)));
+    } else {
+#pragma unroll
+      for (int k = 0; k < 16; ++k) v[k] = 4 * g4 + k < 4ull * groups ? s[4 * g4 + k] : (uint8_t)0;
+    }
+    uint8_t b[12];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t x = ((uint32_t)v[4 * k] << 18) | ((uint32_t)v[4 * k + 1] << 12) | ((uint32_t)v[4 * k + 2] << 6) |
+                         v[4 * k + 3];
+      b[3 * k] = (uint8_t)(x >> 16);
+      b[3 * k + 1] = (uint8_t)(x >> 8);
+      b[3 * k + 2] = (uint8_t)x;
+    }
+    const uint64_t at = 3ull * g4;
+    const uint32_t nb = (uint32_t)min<uint64_t>(12, 3ull * (groups - g4));
+    if (nb == 12 && at + 12 <= limit && (reinterpret_cast<uintptr_t>(o + at) & 3u) == 0) {
+      uint32_t* d = reinterpret_cast<uint32_t*>(o + at);
+#pragma unroll
+      for (int k = 0; k < 3; ++k)
+        d[k] = (uint32_t)b[4 * k] | ((uint32_t)b[4 * k + 1] << 8) | ((uint32_t)b[4 * k + 2] << 16) |
+               ((uint32_t)b[4 * k + 3] << 24);
+    } else {
+      for (uint32_t k = 0; k < nb && at + k < limit; ++k) o[at + k] = b[k];
+    }
+  }
+  if (threadIdx.x == 0) {
+    if (extra) {
+      const uint32_t a = 4 * groups;
+      const uint32_t x = ((uint32_t)s[a] << 18) | ((uint32_t)s[a + 1] << 12) |
+                         ((uint32_t)(extra == 2 ? s[a + 2] : 0) << 6);
+      const uint64_t at = 3ull * groups;
+      if (at < limit) o[at] = (uint8_t)(x >> 16);
+      if (extra == 2 && at + 1 < limit) o[at + 1] = (uint8_t)(x >> 8);
+    }
+    sizes[i] = (uint32_t)min<uint64_t>(want, limit);
+    over[i] = want > limit ? 1 : 0;
+  }
+}
+
+}  // namespace
+}  // namespace lbf

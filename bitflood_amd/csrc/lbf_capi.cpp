@@ -487,6 +487,10 @@ struct Registered {
 struct lbf_ctx {
   std::vector<Worker> workers;
   std::vector<Registered> regs;  // guarded by mu, like every job
+  // lbf_b64_verify_batch's device memory (text, sextets, bytes, tables) on
+  // worker 0's device: one allocation, grown on demand, guarded by mu
+  uint8_t* b64_dev = nullptr;
+  uint64_t b64_cap = 0;
   mutable std::mutex mu;
 };
 
@@ -1350,6 +1354,8 @@ extern "C" int lbf_ctx_worker_info(const lbf_ctx* ctx, int worker, int* device, 
 extern "C" void lbf_ctx_destroy(lbf_ctx* ctx) {
   if (!ctx) return;
   KeepCurrentDevice keep;
+  if (ctx->b64_dev && !ctx->workers.empty() && hipSetDevice(ctx->workers[0].device) == hipSuccess)
+    (void)hipFree(ctx->b64_dev);
   for (Worker& w : ctx->workers) worker_free(w);
   for (const Registered& r : ctx->regs)
     if (r.owned) (void)unpin(r.lo);  // teardown: nowhere to report a failure
@@ -1598,6 +1604,125 @@ extern "C" int lbf_file_ranges(lbf_ctx* ctx, const char* path, const uint64_t* o
                                uint64_t n, const uint8_t* expected, uint8_t* out) {
   if (!ctx || !path) return fail(LBF_ERR_INVALID, "null context/path");
   return lbf_files_ranges(ctx, &path, 1, nullptr, offsets, sizes, n, expected, out);
+}
+
+// Received chunks as base64 text: decode on the device (kern_b64.hpp), then
+// the shipped hash kernels verify the decoded bytes in HBM.  Synchronous on
+// worker 0's first stream: one H2D of the text span and one of the tables, two
+// launches, one D2H of the results and one of the decoded span.
+extern "C" int lbf_b64_verify_batch(lbf_ctx* ctx, const char* text, uint64_t text_len,
+                                    const uint64_t* text_offsets, const uint32_t* text_lens, uint64_t n,
+                                    const uint32_t* expected_sizes, const uint8_t* expected, uint8_t* out,
+                                    uint64_t out_len, const uint64_t* out_offsets, uint32_t* out_sizes,
+                                    uint8_t* verdicts) {
+  if (!ctx) return fail(LBF_ERR_INVALID, "null context");
+  if (n == 0) return LBF_OK;
+  if (!text || !text_offsets || !text_lens || !expected_sizes || !expected || !verdicts)
+    return fail(LBF_ERR_INVALID, "lbf_b64_verify_batch: null argument");
+  if (out && !out_offsets) return fail(LBF_ERR_INVALID, "lbf_b64_verify_batch: out without out_offsets");
+  if (n > 0x7FFFFFFFull) return fail(LBF_ERR_INVALID, "lbf_b64_verify_batch: n too large");
+  uint64_t tlo = UINT64_MAX, thi = 0, olo = UINT64_MAX, ohi = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    if (text_offsets[i] > text_len || text_lens[i] > text_len - text_offsets[i])
+      return fail(LBF_ERR_INVALID, "lbf_b64_verify_batch: text range " + std::to_string(i) + " outside the buffer");
+    tlo = std::min(tlo, text_offsets[i]);
+    thi = std::max(thi, text_offsets[i] + text_lens[i]);
+    if (out) {
+      if (out_offsets[i] > out_len || expected_sizes[i] > out_len - out_offsets[i])
+        return fail(LBF_ERR_INVALID, "lbf_b64_verify_batch: output slot " + std::to_string(i) + " outside the buffer");
+      olo = std::min(olo, out_offsets[i]);
+      ohi = std::max(ohi, out_offsets[i] + expected_sizes[i]);
+    }
+  }
+  // device offsets keep the host offsets' alignment mod 16
+  tlo &= ~15ull;
+  if (out) olo &= ~15ull;
+  return guarded([&] {
+    auto up = [](uint64_t x, uint64_t a) { return (x + a - 1) / a * a; };
+    std::vector<uint64_t> toff(n), soff(n), ooff(n);
+    std::vector<uint32_t> tlen(n), cap(n);
+    uint64_t sext = 0, outb = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+      toff[i] = text_offsets[i] - tlo;
+      soff[i] = sext;
+      sext += up(text_lens[i], 16);
+      tlen[i] = text_lens[i];
+      cap[i] = expected_sizes[i];
+      if (out) {
+        ooff[i] = out_offsets[i] - olo;
+      } else {
+        ooff[i] = outb;
+        outb += up(expected_sizes[i], 16);
+      }
+    }
+    if (out) outb = ohi - olo;
+    // device layout: text | sextets | bytes | inputs (offsets, lengths, caps, expected) | outputs (sizes, over, verdicts)
+    const uint64_t text_b = up(thi - tlo, 256), sext_b = up(sext, 256), out_b = up(outb + 16, 256);
+    const uint64_t in_b = up(n * (8 * 3 + 4 * 2 + 20), 256), res_b = up(n * (4 + 1 + 1), 256);
+    const uint64_t need = text_b + sext_b + out_b + in_b + res_b;
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    KeepCurrentDevice keep;
+    Worker& w = ctx->workers[0];
+    LBF_HIP_TRY(hipSetDevice(w.device));
+    if (need > ctx->b64_cap) {
+      if (ctx->b64_dev) (void)hipFree(ctx->b64_dev);
+      ctx->b64_dev = nullptr;
+      ctx->b64_cap = 0;
+      const uint64_t want = std::max<uint64_t>(need, 64ull << 20);
+      if (hipMalloc(reinterpret_cast<void**>(&ctx->b64_dev), want) != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(LBF_ERR_NOMEM, "lbf_b64_verify_batch: device allocation of " + std::to_string(want) + " bytes");
+      }
+      ctx->b64_cap = want;
+    }
+    uint8_t* d_text = ctx->b64_dev;
+    uint8_t* d_sext = d_text + text_b;
+    uint8_t* d_out = d_sext + sext_b;
+    uint8_t* d_in = d_out + out_b;
+    uint8_t* d_res = d_in + in_b;
+    std::vector<uint8_t> in(n * (8 * 3 + 4 * 2 + 20));
+    uint8_t* q = in.data();
+    auto put = [&](const void* src, uint64_t bytes) {
+      memcpy(q, src, bytes);
+      q += bytes;
+    };
+    put(toff.data(), 8 * n);
+    put(soff.data(), 8 * n);
+    put(ooff.data(), 8 * n);
+    put(tlen.data(), 4 * n);
+    put(cap.data(), 4 * n);
+    put(expected, 20 * n);
+    hipStream_t st = w.dev[0].stream;
+    if (thi > tlo) LBF_HIP_TRY(hipMemcpyAsync(d_text, text + tlo, thi - tlo, hipMemcpyHostToDevice, st));
+    LBF_HIP_TRY(hipMemcpyAsync(d_in, in.data(), in.size(), hipMemcpyHostToDevice, st));
+    const uint64_t* d_toff = reinterpret_cast<const uint64_t*>(d_in);
+    const uint64_t* d_soff = d_toff + n;
+    const uint64_t* d_ooff = d_soff + n;
+    const uint32_t* d_tlen = reinterpret_cast<const uint32_t*>(d_ooff + n);
+    const uint32_t* d_cap = d_tlen + n;
+    const uint8_t* d_exp = reinterpret_cast<const uint8_t*>(d_cap + n);
+    uint32_t* d_sizes = reinterpret_cast<uint32_t*>(d_res);
+    uint8_t* d_over = reinterpret_cast<uint8_t*>(d_sizes + n);
+    uint8_t* d_ver = d_over + n;
+    lbf::B64Launch b{d_text, d_sext, d_toff, d_soff, d_tlen, d_out, d_ooff, d_cap, d_sizes, d_over, (uint32_t)n};
+    if (int rc = lbf::launch_b64_decode(b, st)) return rc;
+    // the decoded lengths are the chunk sizes the hash kernels read
+    if (int rc = lbf_sha1_launch(d_out, d_ooff, d_sizes, n, nullptr, d_exp, d_ver, st)) return rc;
+    std::vector<uint8_t> res(n * 6);
+    LBF_HIP_TRY(hipMemcpyAsync(res.data(), d_res, res.size(), hipMemcpyDeviceToHost, st));
+    if (out && ohi > olo) LBF_HIP_TRY(hipMemcpyAsync(out + olo, d_out, ohi - olo, hipMemcpyDeviceToHost, st));
+    LBF_HIP_TRY(hipStreamSynchronize(st));
+    const uint32_t* sizes = reinterpret_cast<const uint32_t*>(res.data());
+    const uint8_t* over = res.data() + 4 * n;
+    const uint8_t* ver = over + n;
+    for (uint64_t i = 0; i < n; ++i) {
+      // ChunkMethods.cpp:156: the decoded length must be the chunk's size
+      const bool longer = over[i] != 0;
+      verdicts[i] = (ver[i] && !longer && sizes[i] == expected_sizes[i]) ? 1 : 0;
+      if (out_sizes) out_sizes[i] = longer ? expected_sizes[i] + 1 : sizes[i];
+    }
+    return (int)LBF_OK;
+  });
 }
 
 extern "C" int lbf_sha1_one(lbf_ctx* ctx, const uint8_t* data, uint32_t size, uint8_t out[20]) {

@@ -38,6 +38,22 @@ struct ChunkParams {
 int pick_variant(uint64_t n);
 int launch_chunks(const ChunkParams& p, hipStream_t stream);
 
+// Device base64 decode (kern_b64.hpp): n chunks' text -> bytes, on `stream`.
+struct B64Launch {
+  const uint8_t* text;
+  uint8_t* scratch;
+  const uint64_t* text_off;
+  const uint64_t* sext_off;
+  const uint32_t* text_len;
+  uint8_t* out;
+  const uint64_t* out_off;
+  const uint32_t* cap;
+  uint32_t* sizes;
+  uint8_t* over;
+  uint32_t n;
+};
+int launch_b64_decode(const B64Launch& b, hipStream_t stream);
+
 // Kernel variants beyond the shipped ones (1, 7, 10, 11, 12).  Null in the
 // shipped library; the A/B library of tools/experimental/ points it at its
 // superseded and diagnostic variants when it loads.

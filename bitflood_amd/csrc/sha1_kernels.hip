@@ -5,6 +5,8 @@
 // verify hashes of Flood.cpp:259-275 / ChunkMethods.cpp:116-123,165-167 with
 // one batched launch over many independent chunks.
 //
+// Also the receiver's base64 decode (kern_b64.hpp, lbf_b64_verify_batch).
+//
 // Shipped kernels (lbf_kernel_for picks one by chain count):
 //   "lane" (variant 1): one chunk per lane, the simple baseline.  SHA-1 is a
 //     serial Merkle-Damgard chain, so the only parallelism is across chunks;
@@ -35,6 +37,7 @@
 #include "kern_lane.hpp"
 #include "kern_pc.hpp"
 #include "kern_pcx.hpp"
+#include "kern_b64.hpp"
 
 namespace lbf {
 
@@ -172,6 +175,14 @@ int launch_chunks(const ChunkParams& p, hipStream_t stream) {
     if (uniform) launch_lane<true>(p, stream);
     else launch_lane<false>(p, stream);
   }
+  LBF_HIP_TRY(hipGetLastError());
+  return LBF_OK;
+}
+
+int launch_b64_decode(const B64Launch& b, hipStream_t stream) {
+  if (b.n == 0) return LBF_OK;
+  hipLaunchKernelGGL(b64_decode_kernel, dim3(b.n), dim3(kB64Threads), 0, stream, b.text, b.scratch, b.text_off,
+                     b.sext_off, b.text_len, b.out, b.out_off, b.cap, b.sizes, b.over);
   LBF_HIP_TRY(hipGetLastError());
   return LBF_OK;
 }

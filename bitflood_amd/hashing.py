@@ -227,6 +227,41 @@ class ChunkHasher:
         """Resume verify over several files in one batch (Flood.cpp:239-287)."""
         return self._files_call(paths, file_of, offsets, sizes, expected).astype(bool)
 
+    def verify_b64(self, text, text_offsets, text_lens, expected_sizes, expected, out=None, out_offsets=None):
+        """The receiver's decode + verify on the device (lbf_b64_verify_batch,
+        ChunkMethods.cpp:137-167 with xmlrpc++'s base64 decode): chunk i is
+        the base64 text text[text_offsets[i], + text_lens[i]).  Returns
+        (verdicts as bool, decoded lengths); with `out` (a uint8 array) and
+        `out_offsets` the decoded bytes land at out[out_offsets[i], +
+        expected_sizes[i])."""
+        buf = _as_u8(text)
+        toff = np.ascontiguousarray(text_offsets, dtype=np.uint64)
+        tlen = np.ascontiguousarray(text_lens, dtype=np.uint32)
+        esz = np.ascontiguousarray(expected_sizes, dtype=np.uint32)
+        exp = np.ascontiguousarray(expected, dtype=np.uint8).reshape(-1, DIGEST)
+        n = toff.size
+        if not (tlen.size == esz.size == exp.shape[0] == n):
+            raise ValueError("text_offsets, text_lens, expected_sizes and expected differ in length")
+        ver = np.zeros(n, dtype=np.uint8)
+        sizes = np.zeros(n, dtype=np.uint32)
+        if n == 0:
+            return ver.astype(bool), sizes
+        ooff = None
+        if out is not None:
+            if not (isinstance(out, np.ndarray) and out.dtype == np.uint8 and out.flags.c_contiguous):
+                raise ValueError("out must be a C-contiguous uint8 array")
+            ooff = np.ascontiguousarray(out_offsets, dtype=np.uint64)
+            if ooff.size != n:
+                raise ValueError("out_offsets differs in length")
+        base = buf.ctypes.data if buf.size else ctypes.addressof(_EMPTY)
+        check(self._lib.lbf_b64_verify_batch(self._h, base, buf.size, toff.ctypes.data, tlen.ctypes.data, n,
+                                             esz.ctypes.data, exp.ctypes.data,
+                                             None if out is None else out.ctypes.data,
+                                             0 if out is None else out.size,
+                                             None if ooff is None else ooff.ctypes.data, sizes.ctypes.data,
+                                             ver.ctypes.data))
+        return ver.astype(bool), sizes
+
     def sha1(self, data) -> bytes:
         buf = _as_u8(data)
         out = (ctypes.c_uint8 * DIGEST)()

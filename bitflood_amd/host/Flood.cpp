@@ -356,6 +356,55 @@ Error::ErrorCode Flood::VerifyChunks(const U8* i_arena, U64 i_arena_len, const s
   return Error::NO_ERROR_LBF;
 }
 
+// ChunkMethods.cpp:137-167 from the wire form: the base64 decode of the
+// SendChunk payload (XmlRpcValue.cpp:417-436) and the verify, both on the GPU.
+// Chunks whose file or index the flood does not know, whose output slot does
+// not fit the arena, or whose flood-file hash does not decode stay '0'.
+Error::ErrorCode Flood::VerifyTextChunks(const char* i_text, U64 i_text_len, const V_U64& i_text_offsets,
+                                         const V_U32& i_text_lengths, std::vector<ChunkArrival>& io_chunks,
+                                         U8* o_arena, U64 i_arena_len, std::string& o_valid) {
+  const size_t n = io_chunks.size();
+  o_valid.assign(n, '0');
+  if (i_text_offsets.size() != n || i_text_lengths.size() != n) return Error::UNKNOWN_ERROR_LBF;
+  V_U64 toff, ooff;
+  V_U32 tlen, esz;
+  V_U8 vexp;
+  std::vector<size_t> which;
+  for (size_t k = 0; k < n; ++k) {
+    ChunkArrival& a = io_chunks[k];
+    a.m_size = 0;
+    auto it = m_runtimefiles.find(a.m_filename);
+    if (it == m_runtimefiles.end() || a.m_index >= it->second.m_file->m_chunks.size()) continue;
+    const FloodFile::Chunk& c = it->second.m_file->m_chunks[a.m_index];
+    if (a.m_offset > i_arena_len || c.m_size > i_arena_len - a.m_offset) continue;
+    if (i_text_offsets[k] > i_text_len || i_text_lengths[k] > i_text_len - i_text_offsets[k]) continue;
+    U8 e[20];
+    if (!decode_hash(c.m_hash, e)) continue;
+    which.push_back(k);
+    toff.push_back(i_text_offsets[k]);
+    tlen.push_back(i_text_lengths[k]);
+    ooff.push_back(a.m_offset);
+    esz.push_back(c.m_size);
+    vexp.insert(vexp.end(), e, e + 20);
+  }
+  if (which.empty()) return Error::NO_ERROR_LBF;
+  const std::shared_ptr<lbf_ctx> held = Ctx();  // alive for the whole call
+  lbf_ctx* ctx = held.get();
+  if (!ctx) return Error::UNKNOWN_ERROR_LBF;
+  std::vector<U8> verdict(which.size(), 0);
+  V_U32 got(which.size(), 0);
+  if (lbf_b64_verify_batch(ctx, i_text, i_text_len, &toff[0], &tlen[0], which.size(), &esz[0], &vexp[0], o_arena,
+                           i_arena_len, &ooff[0], &got[0], &verdict[0]) != LBF_OK)
+    return Error::UNKNOWN_ERROR_LBF;
+  for (size_t j = 0; j < which.size(); ++j) {
+    // the decoded length, as DecodeSendChunk would report it; a text longer
+    // than the chunk is rejected (ChunkMethods.cpp:156) and writes nothing
+    io_chunks[which[j]].m_size = got[j] <= esz[j] ? got[j] : 0;
+    if (verdict[j]) o_valid[which[j]] = '1';
+  }
+  return Error::NO_ERROR_LBF;
+}
+
 Error::ErrorCode Flood::ReceiveChunks(const U8* i_arena, U64 i_arena_len, const std::vector<ChunkArrival>& i_chunks,
                                       std::string& o_accepted) {
   o_accepted.assign(i_chunks.size(), '0');

@@ -387,5 +387,39 @@ bool DecodeSendChunk(const char* s, size_t len, std::string& o_filename, U32& o_
   return true;
 }
 
+bool LocateSendChunk(const char* s, size_t len, std::string& o_filename, U32& o_index, size_t& o_b64_offset,
+                     size_t& o_b64_length) {
+  const char* a = find(s, len, 0, "<methodName>");
+  if (!a) return false;
+  const size_t b = (size_t)(a - s) + 12;
+  const char* e = find(s, len, b, "</methodName>");
+  if (!e || (size_t)(e - (s + b)) != strlen(kSendChunk) || memcmp(s + b, kSendChunk, strlen(kSendChunk)) != 0)
+    return false;
+  size_t off = (size_t)(e - s) + 13;
+  const char* pp = find(s, len, off, "<params>");
+  if (!pp) return false;
+  off = (size_t)(pp - s) + 8;
+  Value name, idx;
+  if (!next_tag_is("<param>", s, len, off) || !parse_value(s, len, off, name, nullptr, 0, nullptr) ||
+      name.m_type != Value::STRING)
+    return false;
+  next_tag_is("</param>", s, len, off);
+  if (!next_tag_is("<param>", s, len, off) || !parse_value(s, len, off, idx, nullptr, 0, nullptr) ||
+      idx.m_type != Value::INT)
+    return false;
+  next_tag_is("</param>", s, len, off);
+  // parse_value's <base64> branch (binaryFromXml), without the decode
+  if (!next_tag_is("<param>", s, len, off) || !next_tag_is("<value>", s, len, off) ||
+      get_next_tag(s, len, off) != "<base64>")
+    return false;
+  const char* lt = (const char*)memchr(s + off, '<', len - off);
+  if (!lt) return false;
+  o_b64_offset = off;
+  o_b64_length = (size_t)(lt - (s + off));
+  o_filename = name.m_str;
+  o_index = (U32)idx.m_int;
+  return true;
+}
+
 }  // namespace PeerWire
 }  // namespace libBitFlood

@@ -82,6 +82,7 @@ struct Opts {
   bool register_arenas = true;  // --no-register: stage the leecher's verifies (A/B)
   unsigned verifiers = 2;        // leecher: GPU verifies in flight (each its own context)
   bool seeder_pipeline = false;  // --pipelined-seeder: verify batch k+1 while batch k is encoded
+  bool gpu_decode = false;       // --gpu-decode: the leecher's base64 decode on the GPU with its verify
 };
 
 [[noreturn]] void die(const std::string& m) {
@@ -540,12 +541,13 @@ int main(int argc, char** argv) {
     else if (a == "--no-register") o.register_arenas = false;
     else if (a == "--verifiers") o.verifiers = (unsigned)strtoul(val(), nullptr, 10);
     else if (a == "--pipelined-seeder") o.seeder_pipeline = true;
+    else if (a == "--gpu-decode") o.gpu_decode = true;
     else {
       fprintf(stderr,
               "usage: lbf_loopback [--size BYTES] [--chunksize N] [--window W] [--batch B] [--deadline-ms MS]\n"
               "                    [--threads T]\n"
               "                    [--corrupt K] [--dir DIR] [--keep] [--synthetic] [--no-register]\n"
-              "                    [--verifiers V] [--pipelined-seeder]\n");
+              "                    [--verifiers V] [--pipelined-seeder] [--gpu-decode]\n");
       return 2;
     }
   }
@@ -626,6 +628,17 @@ int main(int argc, char** argv) {
   };
   std::vector<Arena> arenas;
   for (int a = 0; a < kArenas; ++a) arenas.push_back(Arena{arena_mem + a * arena_stride, arena_len});
+  // --gpu-decode: each arena has a text arena beside it, where the decode
+  // stage copies the frames' base64 text (one 16-byte aligned slot per
+  // arrival, room for the chunk size's encoded length) for the GPU to decode
+  const U64 text_slot = (PeerWire::Base64PutLength(o.chunksize) + 16 + 15) & ~15ull;
+  const U64 text_len = o.gpu_decode ? text_slot * o.batch : 0;
+  const U64 text_stride = (text_len + page - 1) / page * page;
+  U8* const text_mem = o.gpu_decode ? static_cast<U8*>(aligned_alloc(page, text_stride * kArenas)) : nullptr;
+  if (o.gpu_decode && !text_mem) die("leecher: cannot allocate the text arenas");
+  if (text_mem) memset(text_mem, 0, text_stride * kArenas);
+  std::vector<Arena> texts;
+  for (int a = 0; a < kArenas && text_mem; ++a) texts.push_back(Arena{text_mem + a * text_stride, text_len});
   // One GPU context per verifier, so their verifies run side by side instead of
   // one after another (a context runs one call at a time), each with a copy of
   // the flood's chunk table (VerifyChunks only reads it).  Verifier 0 uses the
@@ -645,9 +658,10 @@ int main(int argc, char** argv) {
   }
   if (o.register_arenas)
     for (lbf_ctx* c : vctx)
-      for (const Arena& a : arenas)
-        if (lbf_host_register(c, a.data(), a.size()) != LBF_OK)
-          die("leecher: lbf_host_register failed: " + std::string(lbf_last_error()));
+      for (const std::vector<Arena>* set : {&arenas, &texts})
+        for (const Arena& a : *set)
+          if (lbf_host_register(c, a.data(), a.size()) != LBF_OK)
+            die("leecher: lbf_host_register failed: " + std::string(lbf_last_error()));
   const int fd = connect_loopback(port);
 
   // Leecher pipeline: reader thread (frames), this thread (decode into one of
@@ -662,6 +676,8 @@ int main(int argc, char** argv) {
     std::vector<Arrival> got;
     std::vector<Flood::ChunkArrival> arr;
     std::vector<size_t> pos;
+    V_U64 text_off;  // --gpu-decode: where each arrival's base64 text lies in its text arena
+    V_U32 text_len;
     int arena = 0;
     std::string acc;
     std::string valid;
@@ -685,9 +701,12 @@ int main(int argc, char** argv) {
       while (to_verify.take(bs, 1)) {
         Batch& b = bs[0];
         auto v0 = Clock::now();
-        if (vfl[v]->VerifyChunks(arenas[b.arena].data(), arenas[b.arena].size(), b.arr, b.valid) !=
-            Error::NO_ERROR_LBF)
-          die("leecher: VerifyChunks failed: " + std::string(Encoder::LastError()));
+        const Error::ErrorCode rc =
+            o.gpu_decode ? vfl[v]->VerifyTextChunks(reinterpret_cast<const char*>(texts[b.arena].data()),
+                                                    texts[b.arena].size(), b.text_off, b.text_len, b.arr,
+                                                    arenas[b.arena].data(), arenas[b.arena].size(), b.valid)
+                         : vfl[v]->VerifyChunks(arenas[b.arena].data(), arenas[b.arena].size(), b.arr, b.valid);
+        if (rc != Error::NO_ERROR_LBF) die("leecher: verify failed: " + std::string(Encoder::LastError()));
         b.verdict = Clock::now();
         b.verify_s = secs(v0, b.verdict);
         --in_gpu;
@@ -813,16 +832,31 @@ int main(int argc, char** argv) {
     b.arena = free_arenas.back();
     free_arenas.pop_back();
     U8* arena = arenas[b.arena].data();
-    // XmlRpcValue::binaryFromXml + the copy loop of :159-163, on `threads` cores
+    // XmlRpcValue::binaryFromXml + the copy loop of :159-163, on `threads` cores;
+    // with --gpu-decode only the frame is parsed here and its base64 text
+    // copied to the text arena: the decode runs on the GPU with the verify
     std::vector<Flood::ChunkArrival> arr(got.size());
     std::vector<char> ok(got.size(), 0);
+    V_U64 toff(got.size(), 0);
+    V_U32 tlen(got.size(), 0);
+    U8* const text = o.gpu_decode ? texts[b.arena].data() : nullptr;
     auto d0 = Clock::now();
     parallel_for(got.size(), o.threads, [&](size_t k) {
       size_t n = 0;
       std::string fname;
       U32 idx = 0;
-      if (PeerWire::DecodeSendChunk(got[k].frame.data(), got[k].frame.size(), fname, idx, arena + k * slot,
-                                    o.chunksize, n)) {
+      if (o.gpu_decode) {
+        size_t at = 0;
+        if (PeerWire::LocateSendChunk(got[k].frame.data(), got[k].frame.size(), fname, idx, at, n) &&
+            n <= text_slot) {
+          memcpy(text + k * text_slot, got[k].frame.data() + at, n);
+          toff[k] = k * text_slot;
+          tlen[k] = (U32)n;
+          arr[k] = Flood::ChunkArrival{fname, idx, k * slot, 0};
+          ok[k] = 1;
+        }
+      } else if (PeerWire::DecodeSendChunk(got[k].frame.data(), got[k].frame.size(), fname, idx, arena + k * slot,
+                                           o.chunksize, n)) {
         arr[k] = Flood::ChunkArrival{fname, idx, k * slot, (U32)n};
         ok[k] = 1;
       }
@@ -833,6 +867,8 @@ int main(int argc, char** argv) {
       if (ok[k]) {
         b.arr.push_back(arr[k]);
         b.pos.push_back(k);
+        b.text_off.push_back(toff[k]);
+        b.text_len.push_back(tlen[k]);
       } else {
         ++undecodable;
       }
@@ -849,10 +885,12 @@ int main(int argc, char** argv) {
   writer.join();
   if (o.register_arenas)
     for (lbf_ctx* c : vctx)
-      for (const Arena& a : arenas) (void)lbf_host_unregister(c, a.data());
+      for (const std::vector<Arena>* set : {&arenas, &texts})
+        for (const Arena& a : *set) (void)lbf_host_unregister(c, a.data());
   vfl.clear();
   for (unsigned v = 1; v < o.verifiers; ++v) lbf_ctx_destroy(vctx[v]);
   free(arena_mem);
+  free(text_mem);
   shutdown(fd, SHUT_RDWR);
   reader.join();
   close(fd);
@@ -874,6 +912,7 @@ int main(int argc, char** argv) {
   const double wall = secs(t_start, t_end);
   printf("{\"config\": \"C5 loopback 2-peer\", \"bytes\": %llu, \"chunk_size\": %u, \"chunks\": %zu, "
          "\"window\": %u, \"batch\": %u, \"deadline_ms\": %u, \"verifiers\": %u, \"seeder_pipelined\": %s, "
+         "\"gpu_decode\": %s, "
          "\"threads\": %u, \"seconds\": %.3f, \"payload_gibs\": %.3f, "
          "\"wire_gibs\": %.3f, \"encode_flood_s\": %.3f, "
          "\"leecher\": {\"batches\": %zu, \"mean_batch\": %.1f, \"decode_s\": %.3f, \"verify_s\": %.3f, "
@@ -884,7 +923,7 @@ int main(int argc, char** argv) {
          "\"resume_verify_complete\": %s, \"files_identical\": %s, \"corrupt_every\": %u, \"corrupted_sent\": %llu, "
          "\"seed_source\": \"%s\", \"arenas_registered\": %s}\n",
          (unsigned long long)o.size, o.chunksize, total, o.window, o.batch, o.deadline_ms, o.verifiers,
-         o.seeder_pipeline ? "true" : "false", o.threads, wall,
+         o.seeder_pipeline ? "true" : "false", o.gpu_decode ? "true" : "false", o.threads, wall,
          payload / wall / (1u << 30), wire_bytes / wall / (1u << 30), encode_s, batches,
          batches ? (double)(accepted + rejected) / batches : 0.0, decode_s, verify_s, write_s, rejected, undecodable,
          (unsigned long long)sst.requests, (unsigned long long)sst.sent, (unsigned long long)sst.refused, sst.verify_s,

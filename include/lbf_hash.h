@@ -147,6 +147,28 @@ int lbf_files_ranges(lbf_ctx* ctx, const char* const* paths, uint32_t n_files, c
                      const uint64_t* offsets, const uint32_t* sizes, uint64_t n, const uint8_t* expected,
                      uint8_t* out);
 
+/* ---- received chunks as base64 text (ChunkMethods.cpp:137-167) -----------
+ * The receiver's two per-chunk passes on the device: XML-RPC's base64 decode
+ * of the SendChunk payload (XmlRpcValue.cpp:417-436, xmlrpc++ 0.7
+ * base64.h:215-330) and the verify.  Chunk i arrived as the base64 text
+ * text[text_offsets[i], + text_lens[i]) (host memory; the bytes between
+ * `<base64>` and `</base64>`).  It is decoded with xmlrpc++'s rules --
+ * characters outside the alphabet are skipped; the first group of four that
+ * holds '=' ends the data ("xx==" one byte, "xxx=" two); an incomplete last
+ * group is dropped -- and verdicts[i] = 1 when the decoded length equals
+ * expected_sizes[i] (ChunkMethods.cpp:156) and its SHA-1 equals
+ * expected[20*i .. 20*i+20).  out_sizes[i] (may be NULL) receives the decoded
+ * length, or expected_sizes[i] + 1 when the text decodes to more.  With `out`
+ * non-NULL the decoded bytes land at out[out_offsets[i], + expected_sizes[i])
+ * (host memory, slots must not overlap); bytes of `out` between the lowest
+ * slot and the end of the highest that are not decoded bytes are unspecified
+ * afterwards.  Synchronous, on the context's first device.  Text and output
+ * in memory registered with lbf_host_register move by DMA without staging. */
+int lbf_b64_verify_batch(lbf_ctx* ctx, const char* text, uint64_t text_len, const uint64_t* text_offsets,
+                         const uint32_t* text_lens, uint64_t n, const uint32_t* expected_sizes,
+                         const uint8_t* expected, uint8_t* out, uint64_t out_len, const uint64_t* out_offsets,
+                         uint32_t* out_sizes, uint8_t* verdicts);
+
 /* ---- single buffer (Encoder::Base64Encode's hash, host memory) ---------- */
 int lbf_sha1_one(lbf_ctx* ctx, const uint8_t* data, uint32_t size, uint8_t out_digest[20]);
 
@@ -172,10 +194,10 @@ int lbf_sha1_uniform_launch(const uint8_t* d_base, uint64_t len, uint32_t chunk_
                             uint64_t first_chunk, uint64_t n, uint8_t* d_digests,
                             const uint8_t* d_expected, uint8_t* d_verdicts, void* stream);
 /* Kernel variant selection for the two launchers above (0 = automatic):
- * shipped are 1 lane, 7 pc4 (schedule read as 8-byte pairs), 10 pcx5 and
- * 11 lds2; the superseded 2 pc, 3 lds, 4 pc2, 5 pcx2, 6 pc4, 8 and 9 pcx4
- * exist only in the LBF_EXPERIMENTAL_VARIANTS build, and the shipped library
- * rejects them with LBF_ERR_INVALID.  Exposed for benchmarking and tests; see
+ * shipped are 1 lane, 7 pc4 (schedule read as 8-byte pairs), 10 pcx5,
+ * 11 lds2 and 12 pc4x2; the superseded and diagnostic variants exist only in
+ * the A/B library of tools/experimental/, and the shipped library rejects
+ * them with LBF_ERR_INVALID.  Exposed for benchmarking and tests; see
  * DESIGN.md "kernels".  lbf_kernel_for(n) is the variant a launch of n
  * chunks runs under the current setting. */
 int lbf_set_kernel_variant(int variant);

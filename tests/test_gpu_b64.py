@@ -1,0 +1,178 @@
+"""The receiver's base64 decode + verify on the device (lbf_b64_verify_batch).
+
+A SendChunk frame carries the chunk as XML-RPC base64 text
+(/root/reference/cpp/src/ChunkMethods.cpp:141-163), written by xmlrpc++ 0.7's
+encoder with a newline after every 18 groups (base64.h:154-210; the frame turns
+it into a space, PeerConnection.cpp:132-156) and read back by its decoder
+(base64.h:215-330).  `b64get` below restates that decoder in Python (the same
+rules bitflood_amd/host/PeerWire.cpp Base64Get restates in C++); the GPU's
+decoded bytes, lengths and verdicts must equal it on well-formed frames of
+every size up to a full C5 chunk and on texts with junk characters, '='
+anywhere, dropped characters and truncation.
+"""
+import base64
+import hashlib
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+EQ, SKIP = 64, 255
+_DEC = np.full(256, SKIP, dtype=np.int16)
+for _i, _c in enumerate(b"ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/"):
+    _DEC[_c] = _i
+_DEC[ord("=")] = EQ
+
+
+def b64get(text: bytes) -> bytes:
+    """xmlrpc++ 0.7 base64 decode (base64.h:215-330): skip characters outside
+    the alphabet; take the rest four at a time; a group holding '=' ends the
+    data ("xx==" one byte, "xxx=" two); an incomplete last group is dropped."""
+    v = _DEC[np.frombuffer(text, dtype=np.uint8)]
+    s = v[v != SKIP]
+    out = bytearray()
+    i = 0
+    while True:
+        if i >= len(s) or s[i] == EQ:
+            return bytes(out)
+        if i + 1 >= len(s) or s[i + 1] == EQ:
+            return bytes(out)
+        c0, c1 = int(s[i]), int(s[i + 1])
+        if i + 2 >= len(s):
+            return bytes(out)
+        c2 = int(s[i + 2])
+        if c2 == EQ:
+            out.append(((c0 << 2) | (c1 >> 4)) & 255)
+            return bytes(out)
+        if i + 3 >= len(s):
+            return bytes(out)
+        c3 = int(s[i + 3])
+        if c3 == EQ:
+            out += bytes([((c0 << 2) | (c1 >> 4)) & 255, ((c1 << 4) | (c2 >> 2)) & 255])
+            return bytes(out)
+        out += bytes([((c0 << 2) | (c1 >> 4)) & 255, ((c1 << 4) | (c2 >> 2)) & 255, ((c2 << 6) | c3) & 255])
+        i += 4
+
+
+def xmlrpc_text(data: bytes) -> bytes:
+    """The payload text of a SendChunk frame: base64 with a newline after
+    every 18th complete group (base64.h:197-205), CR/LF framed as spaces."""
+    s = base64.b64encode(data)
+    full = len(data) // 3
+    parts = []
+    for g in range(len(s) // 4):
+        parts.append(s[4 * g:4 * g + 4])
+        if g < full and g % 18 == 17:
+            parts.append(b" ")
+    return b"".join(parts)
+
+
+def _batch(hasher, texts, datas, align=16, shift=0, with_out=True, sizes=None):
+    """One lbf_b64_verify_batch over texts[i] (expected: datas[i])."""
+    toffs, chunks, pos = [], [], 0
+    for t in texts:
+        pos = (pos + align - 1) // align * align + shift
+        toffs.append(pos)
+        chunks.append((pos, t))
+        pos += len(t)
+    text = np.zeros(pos + 1, dtype=np.uint8)
+    for p, t in chunks:
+        text[p:p + len(t)] = np.frombuffer(t, dtype=np.uint8)
+    esz = np.array([len(d) for d in datas] if sizes is None else sizes, dtype=np.uint32)
+    exp = np.frombuffer(b"".join(hashlib.sha1(d).digest() for d in datas), dtype=np.uint8).reshape(-1, 20)
+    out = ooff = None
+    if with_out:
+        ooff = np.zeros(len(texts), dtype=np.uint64)
+        o = 0
+        for i, s in enumerate(esz):
+            ooff[i] = o
+            o += (int(s) + 15) // 16 * 16
+        out = np.zeros(max(o, 1), dtype=np.uint8)
+    ver, dec = hasher.verify_b64(text, toffs, [len(t) for t in texts], esz, exp, out, ooff)
+    return ver, dec, out, ooff, esz
+
+
+@pytest.mark.parametrize("align,shift", [(16, 0), (16, 3), (1, 0)])
+def test_well_formed_frames_every_size(hasher, align, shift):
+    rng = np.random.default_rng(11 + shift)
+    sizes = [0, 1, 2, 3, 4, 53, 54, 55, 56, 57, 63, 64, 65, 1000, 4095, 65536, 65539, 262144, 262147]
+    datas = [rng.integers(0, 256, n, dtype=np.uint8).tobytes() for n in sizes]
+    texts = [xmlrpc_text(d) for d in datas]
+    ver, dec, out, ooff, esz = _batch(hasher, texts, datas, align, shift)
+    assert ver.all(), np.nonzero(~ver)[0]
+    assert list(dec) == sizes
+    for i, d in enumerate(datas):
+        assert out[int(ooff[i]):int(ooff[i]) + len(d)].tobytes() == d, i
+        if len(d) < 8192:
+            assert b64get(texts[i]) == d  # the restatement agrees with Python's codec
+
+
+def test_perturbed_texts_match_the_reference_decoder(hasher):
+    """Junk characters anywhere, '=' anywhere, characters dropped, truncation:
+    the device's bytes and lengths equal b64get's, and a verdict is 1 exactly
+    when the decoded bytes are the original chunk."""
+    rng = np.random.default_rng(5)
+    junk = [c for c in range(256) if _DEC[c] == SKIP]
+    texts, datas, wants = [], [], []
+    for case in range(400):
+        n = int(rng.integers(0, 3000))
+        d = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        t = bytearray(xmlrpc_text(d))
+        kind = case % 6
+        if kind == 1 and t:  # junk inserted
+            for _ in range(int(rng.integers(1, 20))):
+                t.insert(int(rng.integers(0, len(t) + 1)), int(rng.choice(junk)))
+        elif kind == 2 and t:  # '=' somewhere
+            t.insert(int(rng.integers(0, len(t) + 1)), ord("="))
+        elif kind == 3 and t:  # characters dropped
+            for _ in range(int(rng.integers(1, 4))):
+                if t:
+                    del t[int(rng.integers(0, len(t)))]
+        elif kind == 4:  # truncated
+            t = t[:int(rng.integers(0, len(t) + 1))]
+        elif kind == 5 and t:  # a character flipped to another alphabet character
+            j = int(rng.integers(0, len(t)))
+            if _DEC[t[j]] < 64:
+                t[j] = b"A"[0] if t[j] != b"A"[0] else b"B"[0]
+        texts.append(bytes(t))
+        datas.append(d)
+        wants.append(b64get(bytes(t)))
+    ver, dec, out, ooff, esz = _batch(hasher, texts, datas, align=1, shift=0)
+    for i, (d, w) in enumerate(zip(datas, wants)):
+        cap = len(d)
+        assert int(dec[i]) == (len(w) if len(w) <= cap else cap + 1), (i, len(w), cap, int(dec[i]))
+        got = out[int(ooff[i]):int(ooff[i]) + min(len(w), cap)].tobytes()
+        assert got == w[:cap], i
+        assert bool(ver[i]) == (w == d), i
+
+
+def test_longer_text_and_no_output_buffer(hasher):
+    """A text that decodes to more than the chunk's size fails the size check
+    (ChunkMethods.cpp:156) and reports size + 1; without `out` only the
+    verdicts and lengths come back."""
+    rng = np.random.default_rng(7)
+    d = rng.integers(0, 256, 5000, dtype=np.uint8).tobytes()
+    longer = xmlrpc_text(d + b"xyz")
+    shorter = xmlrpc_text(d[:-3])
+    ver, dec, *_ = _batch(hasher, [longer, shorter, xmlrpc_text(d)], [d, d, d], with_out=False)
+    assert list(ver) == [False, False, True]
+    assert list(dec) == [5001, 4997, 5000]
+
+
+def test_many_chunks_in_one_call(hasher, oracle):
+    """A C5-shaped batch: 300 frames of 64 KiB from the synthetic stream, every
+    tenth corrupted by one flipped alphabet character."""
+    cs, n = 65536, 300
+    data = oracle.synth(0x5EED, 0, cs * n, nthreads=8)
+    datas = [data[i * cs:(i + 1) * cs].tobytes() for i in range(n)]
+    texts = [bytearray(xmlrpc_text(x)) for x in datas]
+    for i in range(0, n, 10):
+        j = 100 + i if texts[i][100 + i] != ord(" ") else 101 + i  # an alphabet character, not a separator
+        texts[i][j] = ord("A") if texts[i][j] != ord("A") else ord("B")
+    ver, dec, out, ooff, esz = _batch(hasher, [bytes(t) for t in texts], datas)
+    assert [bool(v) for v in ver] == [i % 10 != 0 for i in range(n)]
+    assert (dec == cs).all()
+    for i in range(1, n, 37):
+        if i % 10:  # the corrupted ones decode to other bytes, as they should
+            assert out[int(ooff[i]):int(ooff[i]) + cs].tobytes() == datas[i], i

@@ -134,6 +134,8 @@ def test_loopback_two_peers(tmp_path, size, cs, window, batch, corrupt, syntheti
     (["--verifiers", "1", "--pipelined-seeder"], True),
     (["--verifiers", "4"], True),                         # four leecher contexts verifying side by side
     (["--verifiers", "3", "--pipelined-seeder"], False),
+    (["--verifiers", "2", "--gpu-decode"], True),         # base64 decode on the GPU with the verify
+    (["--verifiers", "1", "--gpu-decode"], False),
 ])
 def test_loopback_verifier_counts(tmp_path, extra, synthetic):
     """The leecher's verifiers (each with its own GPU context and a copy of the
@@ -142,6 +144,7 @@ def test_loopback_verifier_counts(tmp_path, extra, synthetic):
     is rejected and fetched again."""
     r = _loopback(tmp_path, (32 << 20) + 12345, 65536, 512, 128, 7, synthetic, extra=extra)
     assert r["verifiers"] == int(extra[1]) and r["seeder_pipelined"] is ("--pipelined-seeder" in extra)
+    assert r["gpu_decode"] is ("--gpu-decode" in extra)
 
 
 @pytest.mark.gpu
