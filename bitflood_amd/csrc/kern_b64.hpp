@@ -23,8 +23,9 @@
 // classifies 16 characters, a workgroup scan gives every valid character its
 // index in S, and the sextets are written to a scratch area laid out like the
 // text.  Pass 2 turns four groups (16 sextets, one 16-byte load) into 12 bytes
-// per lane.  Both passes stream: the bound is HBM (about 4.1 bytes moved per
-// decoded byte: text read, sextets written and read, bytes written).
+// per lane.  Both passes stream: the bound is HBM, 5 bytes moved per decoded
+// byte (4/3 each for the text read and the sextets written and read back, 1
+// for the bytes written).
 //
 // Part of the single translation unit sha1_kernels.hip (included from there).
 #pragma once

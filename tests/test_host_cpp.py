@@ -130,21 +130,22 @@ def test_loopback_two_peers(tmp_path, size, cs, window, batch, corrupt, syntheti
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("extra,synthetic", [
-    (["--verifiers", "1"], False),                        # round 3's shape: one verify in flight
+    (["--verifiers", "1", "--cpu-decode"], False),                         # round 3's shape
     (["--verifiers", "1", "--pipelined-seeder"], True),
-    (["--verifiers", "4"], True),                         # four leecher contexts verifying side by side
-    (["--verifiers", "3", "--pipelined-seeder"], False),
-    (["--verifiers", "2", "--gpu-decode"], True),         # base64 decode on the GPU with the verify
-    (["--verifiers", "1", "--gpu-decode"], False),
+    (["--verifiers", "4"], True),                                          # four leecher contexts side by side
+    (["--verifiers", "3", "--pipelined-seeder", "--cpu-decode"], False),
+    (["--verifiers", "2", "--cpu-decode"], True),                          # the host decode with two verifiers
+    (["--verifiers", "1"], False),
 ])
 def test_loopback_verifier_counts(tmp_path, extra, synthetic):
     """The leecher's verifiers (each with its own GPU context and a copy of the
-    chunk table) and the seeder's verify/encode stages: same end state for
-    every count -- the written file equals the source, every corrupted arrival
-    is rejected and fetched again."""
+    chunk table), its base64 decode on the GPU (the default) or on the host,
+    and the seeder's verify/encode stages: same end state for every
+    combination -- the written file equals the source, every corrupted
+    arrival is rejected and fetched again."""
     r = _loopback(tmp_path, (32 << 20) + 12345, 65536, 512, 128, 7, synthetic, extra=extra)
     assert r["verifiers"] == int(extra[1]) and r["seeder_pipelined"] is ("--pipelined-seeder" in extra)
-    assert r["gpu_decode"] is ("--gpu-decode" in extra)
+    assert r["gpu_decode"] is ("--cpu-decode" not in extra)
 
 
 @pytest.mark.gpu

@@ -1,22 +1,29 @@
 #!/bin/bash
-# tools/c5_ab.sh <tag> <rounds> -- alternating A/B runs of the C5 transfer
+# tools/c5_ab.sh <tag> <rounds> [variants] -- alternating A/B runs of the C5 transfer
 # (16 GiB at 256 KiB, window 4096, batch <= 1024, every 1000th chunk corrupted
 # once, generated seeder) on the GPU box, one JSON line per run appended to
 # gpurun_out/<tag>/c5_ab.jsonl with the variant's name.  Variants (lbf_loopback
 # flags): r03 = one verifier, serial seeder (round 3's pipeline); v1 = one
 # verifier, pipelined seeder; v2 = two verifiers, pipelined seeder; v2s = two
-# verifiers, serial seeder (the default since round 4).
+# verifiers, serial seeder; gd = v2s with the leecher's base64 decode on the
+# GPU (the default since round 4); gd1 = gd with one verifier;
+# pre = v2s run by bitflood_amd/lib/lbf_loopback_prepool when that binary exists
+# (a build of an earlier lbf_loopback.cpp, for an A/B across a harness change).
 set -o pipefail
 tag=${1:-c5ab}
 rounds=${2:-2}
+variants=${3:-"r03 v2 v1 v2s"}
 out=gpurun_out/$tag
 mkdir -p "$out"
 export TMPDIR=${TMPDIR:-/tmp}
-declare -A flags=([r03]="--verifiers 1" [v1]="--verifiers 1 --pipelined-seeder" [v2]="--verifiers 2 --pipelined-seeder" \
-                  [v2s]="--verifiers 2")
+declare -A flags=([r03]="--verifiers 1 --cpu-decode" [v1]="--verifiers 1 --pipelined-seeder --cpu-decode" \
+                  [v2]="--verifiers 2 --pipelined-seeder --cpu-decode" [v2s]="--verifiers 2 --cpu-decode" \
+                  [gd]="--verifiers 2 --gpu-decode" [gd1]="--verifiers 1 --gpu-decode" [pre]="--verifiers 2")
 for r in $(seq "$rounds"); do
-  for v in r03 v2 v1 v2s; do
-    line=$(timeout -k 10 240 bitflood_amd/lib/lbf_loopback --size $((16 << 30)) --chunksize 262144 --window 4096 \
+  for v in $variants; do
+    bin=bitflood_amd/lib/lbf_loopback
+    if [ "$v" = pre ]; then bin=bitflood_amd/lib/lbf_loopback_prepool; fi
+    line=$(timeout -k 10 240 $bin --size $((16 << 30)) --chunksize 262144 --window 4096 \
       --batch 1024 --corrupt 1000 --synthetic --threads 16 --dir "$TMPDIR/c5ab" ${flags[$v]} 2> "$out/$v.$r.err") \
       || { echo "run $v.$r failed rc=$?"; tail -5 "$out/$v.$r.err"; exit 1; }
     echo "{\"variant\": \"$v\", \"round\": $r, \"run\": $line}" >> "$out/c5_ab.jsonl"
