@@ -210,3 +210,57 @@ __global__ void __launch_bounds__(kB64Threads) b64_decode_kernel(const uint8_t* 
 
 }  // namespace
 }  // namespace lbf
+
+namespace lbf {
+namespace {
+
+// ---------------------------------------------------------------------------
+// The sender's base64 encode (lbf_verify_encode_b64_batch): the text a
+// SendChunk frame carries for chunk i, written as xmlrpc++ 0.7's encoder
+// writes it (base64.h:154-210) and as the frame sends it (CR/LF become spaces,
+// PeerConnection.cpp:132-156): four characters per three bytes, a space after
+// every 18th complete group, the last one or two bytes as "xx==" / "xxx=".
+// Group g of chunk i lands at 4g + g/18, so every lane writes its groups
+// independently.  blockIdx.x = chunk; data[data_off[i] .. + size[i]) ->
+// text[text_off[i] .. + b64_put_length(size[i])).
+// ---------------------------------------------------------------------------
+__host__ __device__ constexpr uint64_t b64_put_length(uint64_t size) {
+  return 4 * (size / 3) + (size % 3 ? 4 : 0) + size / 3 / 18;
+}
+
+__global__ void __launch_bounds__(kB64Threads) b64_encode_kernel(const uint8_t* __restrict__ data,
+                                                                 const uint64_t* __restrict__ data_off,
+                                                                 const uint32_t* __restrict__ size,
+                                                                 uint8_t* __restrict__ text,
+                                                                 const uint64_t* __restrict__ text_off) {
+  __shared__ uint8_t alpha[64];
+  if (threadIdx.x < 64) {
+    const uint32_t c = threadIdx.x;
+    alpha[c] = (uint8_t)(c < 26 ? 'A' + c : c < 52 ? 'a' + (c - 26) : c < 62 ? '0' + (c - 52) : c == 62 ? '+' : '/');
+  }
+  __syncthreads();
+  const uint32_t i = blockIdx.x;
+  const uint8_t* d = data + data_off[i];
+  uint8_t* t = text + text_off[i];
+  const uint32_t n = size[i], full = n / 3;
+  for (uint32_t g = threadIdx.x; g < full; g += kB64Threads) {
+    const uint32_t x = ((uint32_t)d[3 * g] << 16) | ((uint32_t)d[3 * g + 1] << 8) | d[3 * g + 2];
+    uint8_t* o = t + 4ull * g + g / 18;
+    o[0] = alpha[x >> 18];
+    o[1] = alpha[(x >> 12) & 63];
+    o[2] = alpha[(x >> 6) & 63];
+    o[3] = alpha[x & 63];
+    if (g % 18 == 17) o[4] = ' ';  // base64.h:197-205's newline, framed as a space
+  }
+  if (threadIdx.x == 0 && n % 3) {
+    uint8_t* o = t + 4ull * full + full / 18;
+    const uint32_t x = ((uint32_t)d[3 * full] << 16) | (n % 3 == 2 ? (uint32_t)d[3 * full + 1] << 8 : 0u);
+    o[0] = alpha[x >> 18];
+    o[1] = alpha[(x >> 12) & 63];
+    o[2] = n % 3 == 2 ? alpha[(x >> 6) & 63] : (uint8_t)'=';
+    o[3] = '=';
+  }
+}
+
+}  // namespace
+}  // namespace lbf

@@ -1606,6 +1606,94 @@ extern "C" int lbf_file_ranges(lbf_ctx* ctx, const char* path, const uint64_t* o
   return lbf_files_ranges(ctx, &path, 1, nullptr, offsets, sizes, n, expected, out);
 }
 
+namespace {
+// The device memory of the two base64 entry points: one allocation on worker
+// 0's device (current when this runs), grown on demand; the caller holds ctx->mu.
+int b64_scratch(lbf_ctx* ctx, uint64_t need, const char* who) {
+  if (need <= ctx->b64_cap) return LBF_OK;
+  if (ctx->b64_dev) (void)hipFree(ctx->b64_dev);
+  ctx->b64_dev = nullptr;
+  ctx->b64_cap = 0;
+  const uint64_t want = std::max<uint64_t>(need, 64ull << 20);
+  if (hipMalloc(reinterpret_cast<void**>(&ctx->b64_dev), want) != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(LBF_ERR_NOMEM, std::string(who) + ": device allocation of " + std::to_string(want) + " bytes");
+  }
+  ctx->b64_cap = want;
+  return LBF_OK;
+}
+}  // namespace
+
+extern "C" uint64_t lbf_b64_put_length(uint64_t size) { return 4 * (size / 3) + (size % 3 ? 4 : 0) + size / 3 / 18; }
+
+// Chunks to send: verify on the device (ChunkMethods.cpp:116-123), then encode
+// each as the base64 text of its SendChunk frame (kern_b64.hpp), from the same
+// device copy.  Synchronous on worker 0's first stream: one H2D of the bytes'
+// span and one of the tables, two launches, one D2H of the verdicts and one of
+// the text span.
+extern "C" int lbf_verify_encode_b64_batch(lbf_ctx* ctx, const uint8_t* data, uint64_t data_len,
+                                           const uint64_t* offsets, const uint32_t* sizes, uint64_t n,
+                                           const uint8_t* expected, uint8_t* verdicts, char* text, uint64_t text_len,
+                                           const uint64_t* text_offsets) {
+  if (!ctx) return fail(LBF_ERR_INVALID, "null context");
+  if (n == 0) return LBF_OK;
+  if (!data || !offsets || !sizes || !expected || !verdicts || !text || !text_offsets)
+    return fail(LBF_ERR_INVALID, "lbf_verify_encode_b64_batch: null argument");
+  if (n > 0x7FFFFFFFull) return fail(LBF_ERR_INVALID, "lbf_verify_encode_b64_batch: n too large");
+  uint64_t dlo = UINT64_MAX, dhi = 0, tlo = UINT64_MAX, thi = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    if (offsets[i] > data_len || sizes[i] > data_len - offsets[i])
+      return fail(LBF_ERR_INVALID, "lbf_verify_encode_b64_batch: chunk " + std::to_string(i) + " outside the buffer");
+    const uint64_t tl = lbf_b64_put_length(sizes[i]);
+    if (text_offsets[i] > text_len || tl > text_len - text_offsets[i])
+      return fail(LBF_ERR_INVALID, "lbf_verify_encode_b64_batch: text slot " + std::to_string(i) + " outside the buffer");
+    dlo = std::min(dlo, offsets[i]);
+    dhi = std::max(dhi, offsets[i] + sizes[i]);
+    tlo = std::min(tlo, text_offsets[i]);
+    thi = std::max(thi, text_offsets[i] + tl);
+  }
+  dlo &= ~15ull;  // device offsets keep the host offsets' alignment mod 16
+  tlo &= ~15ull;
+  return guarded([&] {
+    auto up = [](uint64_t x, uint64_t a) { return (x + a - 1) / a * a; };
+    std::vector<uint8_t> in(n * (8 + 8 + 4 + 20));
+    uint64_t* doff = reinterpret_cast<uint64_t*>(in.data());
+    uint64_t* toff = doff + n;
+    uint32_t* sz = reinterpret_cast<uint32_t*>(toff + n);
+    for (uint64_t i = 0; i < n; ++i) {
+      doff[i] = offsets[i] - dlo;
+      toff[i] = text_offsets[i] - tlo;
+      sz[i] = sizes[i];
+    }
+    memcpy(sz + n, expected, 20 * n);
+    // device layout: bytes | text | inputs (offsets, text offsets, sizes, expected) | verdicts
+    const uint64_t data_b = up(dhi - dlo + 16, 256), text_b = up(thi - tlo + 16, 256), in_b = up(in.size(), 256);
+    const uint64_t need = data_b + text_b + in_b + up(n, 256);
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    KeepCurrentDevice keep;
+    Worker& w = ctx->workers[0];
+    LBF_HIP_TRY(hipSetDevice(w.device));
+    if (int rc = b64_scratch(ctx, need, "lbf_verify_encode_b64_batch")) return rc;
+    uint8_t* d_data = ctx->b64_dev;
+    uint8_t* d_text = d_data + data_b;
+    uint8_t* d_in = d_text + text_b;
+    uint8_t* d_ver = d_in + in_b;
+    hipStream_t st = w.dev[0].stream;
+    if (dhi > dlo) LBF_HIP_TRY(hipMemcpyAsync(d_data, data + dlo, dhi - dlo, hipMemcpyHostToDevice, st));
+    LBF_HIP_TRY(hipMemcpyAsync(d_in, in.data(), in.size(), hipMemcpyHostToDevice, st));
+    const uint64_t* d_doff = reinterpret_cast<const uint64_t*>(d_in);
+    const uint64_t* d_toff = d_doff + n;
+    const uint32_t* d_sz = reinterpret_cast<const uint32_t*>(d_toff + n);
+    const uint8_t* d_exp = reinterpret_cast<const uint8_t*>(d_sz + n);
+    if (int rc = lbf_sha1_launch(d_data, d_doff, d_sz, n, nullptr, d_exp, d_ver, st)) return rc;
+    if (int rc = lbf::launch_b64_encode(d_data, d_doff, d_sz, d_text, d_toff, (uint32_t)n, st)) return rc;
+    LBF_HIP_TRY(hipMemcpyAsync(verdicts, d_ver, n, hipMemcpyDeviceToHost, st));
+    if (thi > tlo) LBF_HIP_TRY(hipMemcpyAsync(text + tlo, d_text, thi - tlo, hipMemcpyDeviceToHost, st));
+    LBF_HIP_TRY(hipStreamSynchronize(st));
+    return (int)LBF_OK;
+  });
+}
+
 // Received chunks as base64 text: decode on the device (kern_b64.hpp), then
 // the shipped hash kernels verify the decoded bytes in HBM.  Synchronous on
 // worker 0's first stream: one H2D of the text span and one of the tables, two
@@ -1664,17 +1752,7 @@ extern "C" int lbf_b64_verify_batch(lbf_ctx* ctx, const char* text, uint64_t tex
     KeepCurrentDevice keep;
     Worker& w = ctx->workers[0];
     LBF_HIP_TRY(hipSetDevice(w.device));
-    if (need > ctx->b64_cap) {
-      if (ctx->b64_dev) (void)hipFree(ctx->b64_dev);
-      ctx->b64_dev = nullptr;
-      ctx->b64_cap = 0;
-      const uint64_t want = std::max<uint64_t>(need, 64ull << 20);
-      if (hipMalloc(reinterpret_cast<void**>(&ctx->b64_dev), want) != hipSuccess) {
-        (void)hipGetLastError();
-        return fail(LBF_ERR_NOMEM, "lbf_b64_verify_batch: device allocation of " + std::to_string(want) + " bytes");
-      }
-      ctx->b64_cap = want;
-    }
+    if (int rc = b64_scratch(ctx, need, "lbf_b64_verify_batch")) return rc;
     uint8_t* d_text = ctx->b64_dev;
     uint8_t* d_sext = d_text + text_b;
     uint8_t* d_out = d_sext + sext_b;

@@ -53,6 +53,9 @@ struct B64Launch {
   uint32_t n;
 };
 int launch_b64_decode(const B64Launch& b, hipStream_t stream);
+// Device base64 encode (kern_b64.hpp): n chunks' bytes -> their SendChunk text.
+int launch_b64_encode(const uint8_t* data, const uint64_t* data_off, const uint32_t* size, uint8_t* text,
+                      const uint64_t* text_off, uint32_t n, hipStream_t stream);
 
 // Kernel variants beyond the shipped ones (1, 7, 10, 11, 12).  Null in the
 // shipped library; the A/B library of tools/experimental/ points it at its

@@ -187,6 +187,14 @@ int launch_b64_decode(const B64Launch& b, hipStream_t stream) {
   return LBF_OK;
 }
 
+int launch_b64_encode(const uint8_t* data, const uint64_t* data_off, const uint32_t* size, uint8_t* text,
+                      const uint64_t* text_off, uint32_t n, hipStream_t stream) {
+  if (n == 0) return LBF_OK;
+  hipLaunchKernelGGL(b64_encode_kernel, dim3(n), dim3(kB64Threads), 0, stream, data, data_off, size, text, text_off);
+  LBF_HIP_TRY(hipGetLastError());
+  return LBF_OK;
+}
+
 }  // namespace lbf
 
 using lbf::fail;

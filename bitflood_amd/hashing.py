@@ -262,6 +262,34 @@ class ChunkHasher:
                                              ver.ctypes.data))
         return ver.astype(bool), sizes
 
+    def verify_encode_b64(self, data, offsets, sizes, expected):
+        """The sender's verify + encode on the device
+        (lbf_verify_encode_b64_batch, ChunkMethods.cpp:89-135 with xmlrpc++'s
+        base64 encode): chunk i = data[offsets[i], + sizes[i]).  Returns
+        (verdicts as bool, [text of chunk i as bytes])."""
+        buf = _as_u8(data)
+        offs = np.ascontiguousarray(offsets, dtype=np.uint64)
+        sz = np.ascontiguousarray(sizes, dtype=np.uint32)
+        exp = np.ascontiguousarray(expected, dtype=np.uint8).reshape(-1, DIGEST)
+        n = offs.size
+        if not (sz.size == exp.shape[0] == n):
+            raise ValueError("offsets, sizes and expected differ in length")
+        ver = np.zeros(n, dtype=np.uint8)
+        if n == 0:
+            return ver.astype(bool), []
+        lens = [int(self._lib.lbf_b64_put_length(int(s))) for s in sz]
+        toff = np.zeros(n, dtype=np.uint64)
+        pos = 0
+        for i, tl in enumerate(lens):
+            toff[i] = pos
+            pos += (tl + 15) // 16 * 16
+        text = np.zeros(max(pos, 1), dtype=np.uint8)
+        base = buf.ctypes.data if buf.size else ctypes.addressof(_EMPTY)
+        check(self._lib.lbf_verify_encode_b64_batch(self._h, base, buf.size, offs.ctypes.data, sz.ctypes.data, n,
+                                                    exp.ctypes.data, ver.ctypes.data, text.ctypes.data, text.size,
+                                                    toff.ctypes.data))
+        return ver.astype(bool), [text[int(toff[i]):int(toff[i]) + lens[i]].tobytes() for i in range(n)]
+
     def sha1(self, data) -> bytes:
         buf = _as_u8(data)
         out = (ctypes.c_uint8 * DIGEST)()

@@ -169,6 +169,24 @@ int lbf_b64_verify_batch(lbf_ctx* ctx, const char* text, uint64_t text_len, cons
                          const uint8_t* expected, uint8_t* out, uint64_t out_len, const uint64_t* out_offsets,
                          uint32_t* out_sizes, uint8_t* verdicts);
 
+/* ---- chunks to send, encoded as base64 text (ChunkMethods.cpp:89-135) ----
+ * The sender's per-chunk passes on the device: the seeder's re-verify
+ * (ChunkMethods.cpp:116-123) and XML-RPC's base64 encode of the SendChunk
+ * payload (XmlRpcValue::binaryToXml, xmlrpc++ 0.7 base64.h:154-210), from one
+ * device copy of the bytes.  Chunk i = data[offsets[i], + sizes[i]) (host
+ * memory): verdicts[i] = 1 when its SHA-1 equals expected[20*i .. 20*i+20);
+ * its text -- four characters per three bytes, a space (the frame's newline)
+ * after every 18th complete group, "xx==" / "xxx=" for a last one or two
+ * bytes -- lands at text[text_offsets[i], + lbf_b64_put_length(sizes[i]))
+ * whatever the verdict.  Bytes of `text` between the lowest slot and the end
+ * of the highest that are not written text are unspecified afterwards.
+ * Synchronous, on the context's first device. */
+int lbf_verify_encode_b64_batch(lbf_ctx* ctx, const uint8_t* data, uint64_t data_len, const uint64_t* offsets,
+                                const uint32_t* sizes, uint64_t n, const uint8_t* expected, uint8_t* verdicts,
+                                char* text, uint64_t text_len, const uint64_t* text_offsets);
+/* Length of that text for a chunk of `size` bytes (xmlrpc++'s encoder). */
+uint64_t lbf_b64_put_length(uint64_t size);
+
 /* ---- single buffer (Encoder::Base64Encode's hash, host memory) ---------- */
 int lbf_sha1_one(lbf_ctx* ctx, const uint8_t* data, uint32_t size, uint8_t out_digest[20]);
 

@@ -176,3 +176,27 @@ def test_many_chunks_in_one_call(hasher, oracle):
     for i in range(1, n, 37):
         if i % 10:  # the corrupted ones decode to other bytes, as they should
             assert out[int(ooff[i]):int(ooff[i]) + cs].tobytes() == datas[i], i
+
+
+def test_sender_encode_matches_xmlrpc_text(hasher):
+    """lbf_verify_encode_b64_batch: the text equals the encoder's (base64.h:154-210,
+    spaces for the frame's newlines) at every size and alignment, and the
+    verdicts mark the chunks whose expected digest is wrong."""
+    rng = np.random.default_rng(21)
+    sizes = [0, 1, 2, 3, 4, 53, 54, 55, 56, 57, 63, 64, 65, 1000, 4095, 65536, 65539, 262144, 262147]
+    offs, pos = [], 0
+    for k, n in enumerate(sizes):
+        pos += k % 5  # ragged starts
+        offs.append(pos)
+        pos += n
+    data = rng.integers(0, 256, pos, dtype=np.uint8)
+    datas = [data[o:o + n].tobytes() for o, n in zip(offs, sizes)]
+    exp = np.frombuffer(b"".join(hashlib.sha1(d).digest() for d in datas), dtype=np.uint8).reshape(-1, 20).copy()
+    exp[3, 0] ^= 1
+    ver, texts = hasher.verify_encode_b64(data, offs, sizes, exp)
+    assert [bool(v) for v in ver] == [i != 3 for i in range(len(sizes))]
+    for i, d in enumerate(datas):
+        assert texts[i] == xmlrpc_text(d), (i, len(d))
+    # round trip through the receiver's device decode
+    rv, rs, out, ooff, _ = _batch(hasher, texts, datas)
+    assert rv.all() and list(rs) == sizes
