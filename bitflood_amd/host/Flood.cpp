@@ -356,6 +356,52 @@ Error::ErrorCode Flood::VerifyChunks(const U8* i_arena, U64 i_arena_len, const s
   return Error::NO_ERROR_LBF;
 }
 
+// ChunkMethods.cpp:116-123 and the encode of its SendChunk payload
+// (XmlRpcValue::binaryToXml), both on the GPU from one device copy: chunk k's
+// base64 text lands at o_text + i_text_offsets[k] (lbf_b64_put_length of its
+// size) whatever its verdict.  Chunks VerifyChunks would skip stay '0' and get
+// no text.
+Error::ErrorCode Flood::VerifyEncodeChunks(const U8* i_arena, U64 i_arena_len, const std::vector<ChunkArrival>& i_chunks,
+                                           std::string& o_valid, char* o_text, U64 i_text_len,
+                                           const V_U64& i_text_offsets) {
+  const size_t n = i_chunks.size();
+  o_valid.assign(n, '0');
+  if (i_text_offsets.size() != n) return Error::UNKNOWN_ERROR_LBF;
+  V_U64 voff, toff;
+  V_U32 vsz;
+  V_U8 vexp;
+  std::vector<size_t> which;
+  for (size_t k = 0; k < n; ++k) {
+    const ChunkArrival& a = i_chunks[k];
+    auto it = m_runtimefiles.find(a.m_filename);
+    if (it == m_runtimefiles.end() || a.m_index >= it->second.m_file->m_chunks.size()) continue;
+    const FloodFile::Chunk& c = it->second.m_file->m_chunks[a.m_index];
+    if (c.m_size != a.m_size) continue;
+    if (a.m_offset > i_arena_len || a.m_size > i_arena_len - a.m_offset) continue;
+    const U64 tl = lbf_b64_put_length(a.m_size);
+    if (i_text_offsets[k] > i_text_len || tl > i_text_len - i_text_offsets[k]) continue;
+    U8 e[20];
+    if (!decode_hash(c.m_hash, e)) continue;
+    which.push_back(k);
+    voff.push_back(a.m_offset);
+    vsz.push_back(a.m_size);
+    toff.push_back(i_text_offsets[k]);
+    vexp.insert(vexp.end(), e, e + 20);
+  }
+  if (which.empty()) return Error::NO_ERROR_LBF;
+  const std::shared_ptr<lbf_ctx> held = Ctx();  // alive for the whole call
+  lbf_ctx* ctx = held.get();
+  if (!ctx) return Error::UNKNOWN_ERROR_LBF;
+  std::vector<U8> verdict(which.size(), 0);
+  static const U8 kEmpty = 0;
+  if (lbf_verify_encode_b64_batch(ctx, i_arena_len ? i_arena : &kEmpty, i_arena_len, &voff[0], &vsz[0], which.size(),
+                                  &vexp[0], &verdict[0], o_text, i_text_len, &toff[0]) != LBF_OK)
+    return Error::UNKNOWN_ERROR_LBF;
+  for (size_t j = 0; j < which.size(); ++j)
+    if (verdict[j]) o_valid[which[j]] = '1';
+  return Error::NO_ERROR_LBF;
+}
+
 // ChunkMethods.cpp:137-167 from the wire form: the base64 decode of the
 // SendChunk payload (XmlRpcValue.cpp:417-436) and the verify, both on the GPU.
 // Chunks whose file or index the flood does not know, whose output slot does

@@ -333,6 +333,31 @@ std::string EncodeSendChunk(const std::string& filename, U32 index, const U8* da
   return s;
 }
 
+std::string FrameSendChunkText(const std::string& filename, U32 index, const char* text, size_t len) {
+  char idx[32];
+  snprintf(idx, sizeof(idx), "%d", (int)index);
+  std::string s;
+  s.reserve(len + filename.size() + 256);
+  s += kRequestBegin;
+  s += kSendChunk;
+  s += kRequestEndMethodName;
+  s += "<params><param><value>";
+  s += XmlEncode(filename);
+  s += "</value></param><param><value><i4>";
+  s += idx;
+  s += "</i4></value></param><param><value><base64>";
+  for (char& c : s)  // frame()'s newline rule, for the header; the text has none
+    if (c == '\n' || c == '\r') c = ' ';
+  s.append(text, len);
+  const size_t tail = s.size();
+  s += "</base64></value></param></params>";
+  s += kRequestEnd;
+  for (size_t i = tail; i < s.size(); ++i)
+    if (s[i] == '\n' || s[i] == '\r') s[i] = ' ';
+  s += '\n';
+  return s;
+}
+
 bool DecodeMethod(const std::string& f, std::string& o_method, std::vector<Value>& o_params) {
   o_params.clear();
   const char* s = f.data();

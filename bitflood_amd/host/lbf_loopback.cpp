@@ -84,6 +84,7 @@ struct Opts {
   unsigned verifiers = 2;        // leecher: GPU verifies in flight (each its own context)
   bool seeder_pipeline = false;  // --pipelined-seeder: verify batch k+1 while batch k is encoded
   bool gpu_decode = true;        // the leecher's base64 decode on the GPU with its verify (--cpu-decode: on the host)
+  bool gpu_encode = false;       // --gpu-encode: the seeder's base64 encode on the GPU with its verify (--synthetic)
 };
 
 [[noreturn]] void die(const std::string& m) {
@@ -465,6 +466,19 @@ void seeder_main(int lfd, FloodFileSPtr ff, std::string root, const Opts& o, See
       if (o.register_arenas && lbf_host_register(ctx, synth_mem + a * synth_cap, synth_cap) != LBF_OK)
         die("seeder: lbf_host_register failed: " + std::string(lbf_last_error()));
   }
+  // --gpu-encode: each arena's chunks come back from the GPU as base64 text,
+  // one 16-byte aligned slot per chunk, in a text arena of its own
+  const U64 text_slot = (PeerWire::Base64PutLength(o.chunksize) + 15) & ~15ull;
+  const U64 text_cap = o.gpu_encode ? (text_slot * o.batch + page - 1) / page * page : 0;
+  char* text_mem = nullptr;
+  if (o.gpu_encode) {
+    text_mem = static_cast<char*>(aligned_alloc(page, text_cap * kSeedArenas));
+    if (!text_mem) die("seeder: cannot allocate the text arenas");
+    memset(text_mem, 0, text_cap * kSeedArenas);
+    for (int a = 0; a < kSeedArenas; ++a)
+      if (o.register_arenas && lbf_host_register(ctx, text_mem + a * text_cap, text_cap) != LBF_OK)
+        die("seeder: lbf_host_register failed: " + std::string(lbf_last_error()));
+  }
   V_U8 file_arena[kSeedArenas];
   Pool gen_pool(o.threads);                                   // this thread's generate
   std::unique_ptr<Pool> enc_pool_own(o.seeder_pipeline ? new Pool(o.threads) : nullptr);
@@ -472,6 +486,7 @@ void seeder_main(int lfd, FloodFileSPtr ff, std::string root, const Opts& o, See
   struct Verified {
     std::vector<Flood::P_ChunkKey> keys;
     V_U64 offs;
+    V_U64 toffs;  // --gpu-encode: the text slots
     std::string valid;
     int arena = 0;
   };
@@ -497,6 +512,19 @@ void seeder_main(int lfd, FloodFileSPtr ff, std::string root, const Opts& o, See
     std::vector<std::string> out(keys.size());
     enc_pool.run(keys.size(), [&](size_t k) {
       if (v.valid[k] != '1') return;  // "send only if equal" (ChunkMethods.cpp:117-123)
+      if (o.gpu_encode) {  // the GPU's text; a wire error flips one of its characters
+        const char* t = text_mem + v.arena * text_cap + v.toffs[k];
+        const size_t tl = PeerWire::Base64PutLength(sizes[k]);
+        if (!flip[k]) {
+          out[k] = PeerWire::FrameSendChunkText(keys[k].first, keys[k].second, t, tl);
+          return;
+        }
+        std::string tmp(t, tl);
+        const size_t g = sizes[k] / 2 / 3, at = 4 * g + g / 18;  // a character of the middle byte's group
+        tmp[at] = tmp[at] == 'A' ? 'B' : 'A';
+        out[k] = PeerWire::FrameSendChunkText(keys[k].first, keys[k].second, tmp.data(), tl);
+        return;
+      }
       const U8* data = arena + v.offs[k];
       std::vector<U8> tmp;
       if (flip[k]) {  // a wire error after the seeder's own verify
@@ -555,8 +583,15 @@ void seeder_main(int lfd, FloodFileSPtr ff, std::string root, const Opts& o, See
         if (chunks[k].m_size == 0 || it == fl.m_runtimefiles.end()) return;
         synth_bytes(arena + v.offs[k], it->second.m_chunkoffsets[keys[k].second], chunks[k].m_size);
       });
-      if (fl.VerifyChunks(arena, synth_cap, chunks, v.valid) != Error::NO_ERROR_LBF)
+      if (o.gpu_encode) {
+        v.toffs.resize(keys.size());
+        for (size_t k = 0; k < keys.size(); ++k) v.toffs[k] = k * text_slot;
+        if (fl.VerifyEncodeChunks(arena, synth_cap, chunks, v.valid, text_mem + v.arena * text_cap, text_cap,
+                                  v.toffs) != Error::NO_ERROR_LBF)
+          die("seeder: verify + encode failed: " + std::string(Encoder::LastError()));
+      } else if (fl.VerifyChunks(arena, synth_cap, chunks, v.valid) != Error::NO_ERROR_LBF) {
         die("seeder: verify failed: " + std::string(Encoder::LastError()));
+      }
     } else if (fl.ReadVerifiedChunks(keys, file_arena[v.arena], v.offs, v.valid) != Error::NO_ERROR_LBF) {
       die("seeder: verify failed: " + std::string(Encoder::LastError()));
     }
@@ -580,6 +615,11 @@ void seeder_main(int lfd, FloodFileSPtr ff, std::string root, const Opts& o, See
     for (int a = 0; a < kSeedArenas; ++a)
       if (o.register_arenas) (void)lbf_host_unregister(ctx, synth_mem + a * synth_cap);
     free(synth_mem);
+  }
+  if (text_mem) {
+    for (int a = 0; a < kSeedArenas; ++a)
+      if (o.register_arenas) (void)lbf_host_unregister(ctx, text_mem + a * text_cap);
+    free(text_mem);
   }
   lbf_ctx_destroy(ctx);
 }
@@ -616,17 +656,21 @@ int main(int argc, char** argv) {
     else if (a == "--pipelined-seeder") o.seeder_pipeline = true;
     else if (a == "--gpu-decode") o.gpu_decode = true;
     else if (a == "--cpu-decode") o.gpu_decode = false;
+    else if (a == "--gpu-encode") o.gpu_encode = true;
+    else if (a == "--cpu-encode") o.gpu_encode = false;
     else {
       fprintf(stderr,
               "usage: lbf_loopback [--size BYTES] [--chunksize N] [--window W] [--batch B] [--deadline-ms MS]\n"
               "                    [--threads T]\n"
               "                    [--corrupt K] [--dir DIR] [--keep] [--synthetic] [--no-register]\n"
-              "                    [--verifiers V] [--pipelined-seeder] [--gpu-decode | --cpu-decode]\n");
+              "                    [--verifiers V] [--pipelined-seeder] [--gpu-decode | --cpu-decode]\n"
+              "                    [--gpu-encode | --cpu-encode]\n");
       return 2;
     }
   }
   if (o.chunksize == 0 || o.window == 0 || o.batch == 0) die("chunksize, window and batch must be > 0");
   if (o.verifiers == 0 || o.verifiers > 8) die("verifiers must be 1..8");
+  if (o.gpu_encode && !o.synthetic) die("--gpu-encode needs --synthetic (the file seeder reads and verifies in one call)");
   if (o.dir.empty()) {
     const char* t = getenv("TMPDIR");
     char tmpl[512];
@@ -987,7 +1031,7 @@ int main(int argc, char** argv) {
   const double wall = secs(t_start, t_end);
   printf("{\"config\": \"C5 loopback 2-peer\", \"bytes\": %llu, \"chunk_size\": %u, \"chunks\": %zu, "
          "\"window\": %u, \"batch\": %u, \"deadline_ms\": %u, \"verifiers\": %u, \"seeder_pipelined\": %s, "
-         "\"gpu_decode\": %s, "
+         "\"gpu_decode\": %s, \"gpu_encode\": %s, "
          "\"threads\": %u, \"seconds\": %.3f, \"payload_gibs\": %.3f, "
          "\"wire_gibs\": %.3f, \"encode_flood_s\": %.3f, "
          "\"leecher\": {\"batches\": %zu, \"mean_batch\": %.1f, \"decode_s\": %.3f, \"verify_s\": %.3f, "
@@ -998,7 +1042,8 @@ int main(int argc, char** argv) {
          "\"resume_verify_complete\": %s, \"files_identical\": %s, \"corrupt_every\": %u, \"corrupted_sent\": %llu, "
          "\"seed_source\": \"%s\", \"arenas_registered\": %s}\n",
          (unsigned long long)o.size, o.chunksize, total, o.window, o.batch, o.deadline_ms, o.verifiers,
-         o.seeder_pipeline ? "true" : "false", o.gpu_decode ? "true" : "false", o.threads, wall,
+         o.seeder_pipeline ? "true" : "false", o.gpu_decode ? "true" : "false",
+         o.gpu_encode ? "true" : "false", o.threads, wall,
          payload / wall / (1u << 30), wire_bytes / wall / (1u << 30), encode_s, batches,
          batches ? (double)(accepted + rejected) / batches : 0.0, decode_s, verify_s, write_s, rejected, undecodable,
          (unsigned long long)sst.requests, (unsigned long long)sst.sent, (unsigned long long)sst.refused, sst.verify_s,

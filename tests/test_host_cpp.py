@@ -136,6 +136,8 @@ def test_loopback_two_peers(tmp_path, size, cs, window, batch, corrupt, syntheti
     (["--verifiers", "3", "--pipelined-seeder", "--cpu-decode"], False),
     (["--verifiers", "2", "--cpu-decode"], True),                          # the host decode with two verifiers
     (["--verifiers", "1"], False),
+    (["--verifiers", "2", "--gpu-encode"], True),                          # the seeder's encode on the GPU too
+    (["--verifiers", "1", "--gpu-encode", "--pipelined-seeder", "--cpu-decode"], True),
 ])
 def test_loopback_verifier_counts(tmp_path, extra, synthetic):
     """The leecher's verifiers (each with its own GPU context and a copy of the
@@ -146,6 +148,7 @@ def test_loopback_verifier_counts(tmp_path, extra, synthetic):
     r = _loopback(tmp_path, (32 << 20) + 12345, 65536, 512, 128, 7, synthetic, extra=extra)
     assert r["verifiers"] == int(extra[1]) and r["seeder_pipelined"] is ("--pipelined-seeder" in extra)
     assert r["gpu_decode"] is ("--cpu-decode" not in extra)
+    assert r["gpu_encode"] is ("--gpu-encode" in extra)
 
 
 @pytest.mark.gpu

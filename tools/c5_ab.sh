@@ -6,7 +6,8 @@
 # flags): r03 = one verifier, serial seeder (round 3's pipeline); v1 = one
 # verifier, pipelined seeder; v2 = two verifiers, pipelined seeder; v2s = two
 # verifiers, serial seeder; gd = v2s with the leecher's base64 decode on the
-# GPU (the default since round 4); gd1 = gd with one verifier;
+# GPU (the default since round 4); gd1 = gd with one verifier; ge = gd with
+# the seeder's base64 encode on the GPU too (--gpu-encode);
 # pre = v2s run by bitflood_amd/lib/lbf_loopback_prepool when that binary exists
 # (a build of an earlier lbf_loopback.cpp, for an A/B across a harness change).
 set -o pipefail
@@ -18,7 +19,8 @@ mkdir -p "$out"
 export TMPDIR=${TMPDIR:-/tmp}
 declare -A flags=([r03]="--verifiers 1 --cpu-decode" [v1]="--verifiers 1 --pipelined-seeder --cpu-decode" \
                   [v2]="--verifiers 2 --pipelined-seeder --cpu-decode" [v2s]="--verifiers 2 --cpu-decode" \
-                  [gd]="--verifiers 2 --gpu-decode" [gd1]="--verifiers 1 --gpu-decode" [pre]="--verifiers 2")
+                  [gd]="--verifiers 2 --gpu-decode" [gd1]="--verifiers 1 --gpu-decode" \
+                  [ge]="--verifiers 2 --gpu-decode --gpu-encode" [pre]="--verifiers 2")
 for r in $(seq "$rounds"); do
   for v in $variants; do
     bin=bitflood_amd/lib/lbf_loopback
