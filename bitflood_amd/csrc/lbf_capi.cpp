@@ -1627,7 +1627,8 @@ int b64_scratch(lbf_ctx* ctx, uint64_t need, const char* who) {
 extern "C" uint64_t lbf_b64_put_length(uint64_t size) { return 4 * (size / 3) + (size % 3 ? 4 : 0) + size / 3 / 18; }
 
 // Chunks to send: verify on the device (ChunkMethods.cpp:116-123), then encode
-// each as the base64 text of its SendChunk frame (kern_b64.hpp), from the same
+// each as the base64 text of its SendChunk frame (XmlRpcValue.cpp:439-452,
+// kern_b64.hpp), from the same
 // device copy.  Synchronous on worker 0's first stream: one H2D of the bytes'
 // span and one of the tables, two launches, one D2H of the verdicts and one of
 // the text span.

@@ -15,6 +15,7 @@
 
 #include "libBitFlood/Encoder.H"
 #include "libBitFlood/Flood.H"
+#include "libBitFlood/PeerWire.H"
 
 using namespace libBitFlood;
 
@@ -181,6 +182,58 @@ int main(int argc, char** argv) {
   again.m_rootdir = ldir;
   CHECK(again.Initialize(lf) == Error::NO_ERROR_LBF);
   CHECK(again.m_runtimefiles["copy.bin"].m_chunkmap == "1111");
+
+  // the wire form end to end: the seeder's verify + encode on the GPU
+  // (VerifyEncodeChunks) frames the same bytes as EncodeSendChunk; a receiver
+  // decoding those frames on the GPU (VerifyTextChunks) accepts every chunk
+  // but the one whose expected size disagrees and the one flipped on the wire
+  {
+    std::vector<Flood::ChunkArrival> out(5);
+    V_U64 toff(5);
+    for (U32 i = 0; i < 4; ++i) {
+      out[i] = Flood::ChunkArrival{src, i, 65536ull * i, i == 3 ? 777u : 65536u};
+      toff[i] = 90000ull * i;
+    }
+    out[4] = Flood::ChunkArrival{src, 2, 65536ull * 2, 1000};  // wrong size: skipped
+    toff[4] = 90000ull * 4;
+    std::vector<char> text(90000 * 5, 0);
+    std::string ok;
+    CHECK(seeder.VerifyEncodeChunks(data.data(), data.size(), out, ok, text.data(), text.size(), toff) ==
+          Error::NO_ERROR_LBF);
+    CHECK(ok == "11110");
+    std::vector<std::string> frames;
+    for (U32 i = 0; i < 4; ++i) {
+      const U32 sz = out[i].m_size;
+      frames.push_back(PeerWire::FrameSendChunkText(src, i, &text[toff[i]], PeerWire::Base64PutLength(sz)));
+      CHECK(frames.back() == PeerWire::EncodeSendChunk(src, i, data.data() + 65536ull * i, sz));
+    }
+    std::string& f1 = frames[1];  // a character flipped in transit
+    const size_t at = f1.find("<base64>") + 8 + 100;
+    f1[at] = f1[at] == 'A' ? 'B' : 'A';
+    std::string all;
+    V_U64 boff;
+    V_U32 blen;
+    std::vector<Flood::ChunkArrival> got;
+    for (U32 i = 0; i < 4; ++i) {
+      std::string fname;
+      U32 idx = 0;
+      size_t b = 0, n = 0;
+      CHECK(PeerWire::LocateSendChunk(frames[i].data(), frames[i].size(), fname, idx, b, n) && idx == i);
+      boff.push_back(all.size() + b);
+      blen.push_back((U32)n);
+      got.push_back(Flood::ChunkArrival{"copy.bin", idx, 65536ull * i, 0});
+      all += frames[i];
+    }
+    Flood leech2;
+    leech2.m_rootdir = ldir;
+    CHECK(leech2.Initialize(lf) == Error::NO_ERROR_LBF);
+    std::vector<U8> arena(4 * 65536);
+    std::string valid;
+    CHECK(leech2.VerifyTextChunks(all.data(), all.size(), boff, blen, got, arena.data(), arena.size(), valid) ==
+          Error::NO_ERROR_LBF);
+    CHECK(valid == "1011");
+    CHECK(got[3].m_size == 777 && std::memcmp(arena.data() + 3 * 65536, data.data() + 3 * 65536, 777) == 0);
+  }
 
   // multi-file EncodeFile (Encoder.cpp:17-102): every file of m_files, an empty
   // one included (no chunks), keyed by name; the hashes equal the batch path's

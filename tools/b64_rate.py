@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
-"""Rate of lbf_b64_verify_batch (diagnostic, GPU box): N chunks of C5 frames'
-base64 text decoded and verified on the device, against the host decode the
+"""Rate of lbf_b64_verify_batch and lbf_verify_encode_b64_batch (diagnostic,
+GPU box): N chunks of C5 frames' base64 text decoded and verified on the
+device, and N chunks verified and encoded, against the host decode the
 leecher otherwise runs (PeerWire::Base64Get is C++; Python's binascii stands
 in for its rate only as an order of magnitude).  Run it under
 `rocprofv3 --kernel-trace --stats` for the decode kernel's own duration.
@@ -71,6 +72,27 @@ def main():
             v2 = h.verify_chunks(out, ooff, esz, exp)
         dt = (time.perf_counter() - t0) / a.reps
         res["verify_decoded_registered"] = {"ms": round(dt * 1e3, 3), "parity": bool(v2.all())}
+        # the sender's half: verify + encode of the same chunks into the same
+        # text layout (both registered), whole call timed
+        dptr = data.ctypes.data
+        h.register_host(data)
+        enc = np.zeros_like(text)
+        h.register_host(enc)
+        ver = np.zeros(n, dtype=np.uint8)
+        dsz = np.full(n, cs, dtype=np.uint32)
+        args = (h._h, dptr, data.size, ooff.ctypes.data, dsz.ctypes.data, n, exp.ctypes.data, ver.ctypes.data,
+                enc.ctypes.data, enc.size, toff.ctypes.data)
+        assert h._lib.lbf_verify_encode_b64_batch(*args) == 0
+        t0 = time.perf_counter()
+        for _ in range(a.reps):
+            h._lib.lbf_verify_encode_b64_batch(*args)
+        dt = (time.perf_counter() - t0) / a.reps
+        same = all(bytes(enc[i * slot:i * slot + tlen[i]]) == bytes(text[i * slot:i * slot + tlen[i]])
+                   for i in range(0, n, max(1, n // 16)))
+        res["verify_encode_registered"] = {"ms": round(dt * 1e3, 3), "bytes_gibs": round(cs * n / dt / 2**30, 3),
+                                           "parity": bool(ver.all()) and same}
+        h.unregister_host(data)
+        h.unregister_host(enc)
         h.unregister_host(text)
         h.unregister_host(out)
     # host decode of the same text, one thread, for scale (binascii, C)
@@ -79,6 +101,11 @@ def main():
         base64.b64decode(bytes(text[i * slot:i * slot + tlen[i]]).replace(b" ", b""))
     dt = (time.perf_counter() - t0) / min(n, 256)
     res["host_binascii_one_thread_gibs"] = round(cs / dt / 2**30, 3)
+    t0 = time.perf_counter()
+    for i in range(min(n, 256)):
+        base64.b64encode(data[i * cs:(i + 1) * cs])
+    dt = (time.perf_counter() - t0) / min(n, 256)
+    res["host_binascii_encode_one_thread_gibs"] = round(cs / dt / 2**30, 3)
     print(json.dumps(res), flush=True)
 
 
