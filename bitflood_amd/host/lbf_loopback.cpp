@@ -85,6 +85,7 @@ struct Opts {
   bool seeder_pipeline = false;  // --pipelined-seeder: verify batch k+1 while batch k is encoded
   bool gpu_decode = true;        // the leecher's base64 decode on the GPU with its verify (--cpu-decode: on the host)
   bool gpu_encode = false;       // --gpu-encode: the seeder's base64 encode on the GPU with its verify (--synthetic)
+  unsigned seeder_workers = 1;   // --seeder-workers S: the seeder's verify/encode workers (each its own context)
 };
 
 [[noreturn]] void die(const std::string& m) {
@@ -413,23 +414,30 @@ struct Chan {
   }
 };
 
-// Seeder pipeline: reader thread (frames -> request keys), this thread (read +
-// GPU verify + parallel encode of a batch), sender thread (frames -> socket).
-// --pipelined-seeder moves the encode to a thread of its own, so batch k+1 is
-// read and verified while batch k is encoded.  On the 16-CPU GPU box that did
-// not raise the transfer rate and cost latency: the generator and the encoder
-// then compete for the same cores, so it is not the default.
+// Seeder pipeline: reader thread (frames -> request keys), S workers (read +
+// GPU verify + parallel encode of a batch; each its own GPU context, arenas and
+// thread pool, taking whatever requests are queued when it is free), sender
+// thread (frames -> socket).  A batch costs at least one chunk's SHA-1 chain on
+// the GPU (3.1 ms at 256 KiB) however few chains it holds, so a second worker
+// verifies the next requests while the first waits for its chain.
+// --pipelined-seeder moves each worker's encode to a thread of its own, so batch
+// k+1 is read and verified while batch k is encoded.  On the 16-CPU GPU box that
+// did not raise the transfer rate and cost latency: the generator and the
+// encoder then compete for the same cores, so it is not the
+// default.
 void seeder_main(int lfd, FloodFileSPtr ff, std::string root, const Opts& o, SeederStats& st) {
   const int fd = accept(lfd, nullptr, nullptr);
   if (fd < 0) die("accept failed");
   tune(fd);
-  // the seeder is its own peer: its own GPU context (streams, staging)
-  lbf_ctx* ctx = nullptr;
-  if (lbf_ctx_create(0, &ctx) != LBF_OK) die(std::string("seeder: lbf_ctx_create: ") + lbf_last_error());
-  Flood fl;
-  fl.m_rootdir = root;
-  fl.m_ctx = ctx;
-  if (fl.Initialize(ff) != Error::NO_ERROR_LBF) die("seeder: Initialize failed: " + std::string(Encoder::LastError()));
+  // the seeder is its own peer: its own GPU contexts (streams, staging), one per
+  // worker, and one resume verify whose result every worker copies
+  std::vector<lbf_ctx*> wctx(o.seeder_workers, nullptr);
+  for (unsigned w = 0; w < o.seeder_workers; ++w)
+    if (lbf_ctx_create(0, &wctx[w]) != LBF_OK) die(std::string("seeder: lbf_ctx_create: ") + lbf_last_error());
+  Flood fl0;
+  fl0.m_rootdir = root;
+  fl0.m_ctx = wctx[0];
+  if (fl0.Initialize(ff) != Error::NO_ERROR_LBF) die("seeder: Initialize failed: " + std::string(Encoder::LastError()));
   Chan<Flood::P_ChunkKey> requests;
   Chan<std::string> outbox;
   std::thread reader([&] {
@@ -448,180 +456,206 @@ void seeder_main(int lfd, FloodFileSPtr ff, std::string root, const Opts& o, See
     while (outbox.take(msgs, 64))
       for (const std::string& m : msgs) ok = ok && send_all(fd, m);
   });
-  // Two arenas for the whole transfer (one being verified, one being encoded),
-  // page-aligned and (unless --no-register) registered with the seeder's
-  // context, like the leecher's: a batch costs no allocation, no zero fill of up
-  // to batch x chunk bytes, and no staging copy on its verify.
-  // ReadVerifiedChunks keeps its own vectors the same way.
-  constexpr int kSeedArenas = 2;
+  std::mutex shared_mu;          // the workers' shared state below
+  Flood::S_ChunkKey corrupted;   // chunks already sent corrupted once
   const U64 page = (U64)sysconf(_SC_PAGESIZE);
   const U64 slot_bytes = ((U64)o.chunksize + 15) & ~15ull;
   const U64 synth_cap = (slot_bytes * o.batch + page - 1) / page * page;
-  U8* synth_mem = nullptr;
-  if (o.synthetic) {
-    synth_mem = static_cast<U8*>(aligned_alloc(page, synth_cap * kSeedArenas));
-    if (!synth_mem) die("seeder: cannot allocate the arenas");
-    memset(synth_mem, 0, synth_cap * kSeedArenas);
-    for (int a = 0; a < kSeedArenas; ++a)
-      if (o.register_arenas && lbf_host_register(ctx, synth_mem + a * synth_cap, synth_cap) != LBF_OK)
-        die("seeder: lbf_host_register failed: " + std::string(lbf_last_error()));
-  }
   // --gpu-encode: each arena's chunks come back from the GPU as base64 text,
   // one 16-byte aligned slot per chunk, in a text arena of its own
   const U64 text_slot = (PeerWire::Base64PutLength(o.chunksize) + 15) & ~15ull;
   const U64 text_cap = o.gpu_encode ? (text_slot * o.batch + page - 1) / page * page : 0;
-  char* text_mem = nullptr;
-  if (o.gpu_encode) {
-    text_mem = static_cast<char*>(aligned_alloc(page, text_cap * kSeedArenas));
-    if (!text_mem) die("seeder: cannot allocate the text arenas");
-    memset(text_mem, 0, text_cap * kSeedArenas);
-    for (int a = 0; a < kSeedArenas; ++a)
-      if (o.register_arenas && lbf_host_register(ctx, text_mem + a * text_cap, text_cap) != LBF_OK)
-        die("seeder: lbf_host_register failed: " + std::string(lbf_last_error()));
-  }
-  V_U8 file_arena[kSeedArenas];
-  Pool gen_pool(o.threads);                                   // this thread's generate
-  std::unique_ptr<Pool> enc_pool_own(o.seeder_pipeline ? new Pool(o.threads) : nullptr);
-  Pool& enc_pool = o.seeder_pipeline ? *enc_pool_own : gen_pool;  // the encode stage's
-  struct Verified {
-    std::vector<Flood::P_ChunkKey> keys;
-    V_U64 offs;
-    V_U64 toffs;  // --gpu-encode: the text slots
-    std::string valid;
-    int arena = 0;
-  };
-  Chan<Verified> to_encode;
-  Chan<int> free_arena;
-  for (int a = 0; a < kSeedArenas; ++a) free_arena.put(a);
-  Flood::S_ChunkKey corrupted;  // the encode stage's alone
-  auto encode = [&](Verified& v) {
-    const std::vector<Flood::P_ChunkKey>& keys = v.keys;
-    const U8* arena = o.synthetic ? synth_mem + v.arena * synth_cap : file_arena[v.arena].data();
-    auto t1 = Clock::now();
-    // sizes and the (first-send-only) corruption decision, serially
-    std::vector<U32> sizes(keys.size(), 0);
-    std::vector<char> flip(keys.size(), 0);
-    for (size_t k = 0; k < keys.size(); ++k) {
-      if (v.valid[k] != '1') continue;
-      sizes[k] = fl.m_runtimefiles.find(keys[k].first)->second.m_file->m_chunks[keys[k].second].m_size;
-      if (o.corrupt && sizes[k] && keys[k].second % o.corrupt == o.corrupt - 1 && corrupted.insert(keys[k]).second) {
-        flip[k] = 1;
-        ++st.corrupted;
-      }
+  const unsigned pool_threads = std::max(1u, o.threads / o.seeder_workers);
+  auto worker = [&](unsigned w) {
+    lbf_ctx* ctx = wctx[w];
+    Flood fl;
+    fl.m_floodfile = fl0.m_floodfile;
+    fl.m_runtimefiles = fl0.m_runtimefiles;
+    fl.m_rootdir = fl0.m_rootdir;
+    fl.m_ctx = ctx;
+    SeederStats mine;
+    // Two arenas per worker (one being verified, one being encoded),
+    // page-aligned and (unless --no-register) registered with the worker's
+    // context, like the leecher's: a batch costs no allocation, no zero fill of
+    // up to batch x chunk bytes, and no staging copy on its verify.
+    // ReadVerifiedChunks keeps its own vectors the same way.
+    constexpr int kSeedArenas = 2;
+    U8* synth_mem = nullptr;
+    if (o.synthetic) {
+      synth_mem = static_cast<U8*>(aligned_alloc(page, synth_cap * kSeedArenas));
+      if (!synth_mem) die("seeder: cannot allocate the arenas");
+      memset(synth_mem, 0, synth_cap * kSeedArenas);
+      for (int a = 0; a < kSeedArenas; ++a)
+        if (o.register_arenas && lbf_host_register(ctx, synth_mem + a * synth_cap, synth_cap) != LBF_OK)
+          die("seeder: lbf_host_register failed: " + std::string(lbf_last_error()));
     }
-    std::vector<std::string> out(keys.size());
-    enc_pool.run(keys.size(), [&](size_t k) {
-      if (v.valid[k] != '1') return;  // "send only if equal" (ChunkMethods.cpp:117-123)
-      if (o.gpu_encode) {  // the GPU's text; a wire error flips one of its characters
-        const char* t = text_mem + v.arena * text_cap + v.toffs[k];
-        const size_t tl = PeerWire::Base64PutLength(sizes[k]);
-        if (!flip[k]) {
-          out[k] = PeerWire::FrameSendChunkText(keys[k].first, keys[k].second, t, tl);
+    char* text_mem = nullptr;
+    if (o.gpu_encode) {
+      text_mem = static_cast<char*>(aligned_alloc(page, text_cap * kSeedArenas));
+      if (!text_mem) die("seeder: cannot allocate the text arenas");
+      memset(text_mem, 0, text_cap * kSeedArenas);
+      for (int a = 0; a < kSeedArenas; ++a)
+        if (o.register_arenas && lbf_host_register(ctx, text_mem + a * text_cap, text_cap) != LBF_OK)
+          die("seeder: lbf_host_register failed: " + std::string(lbf_last_error()));
+    }
+    V_U8 file_arena[kSeedArenas];
+    Pool gen_pool(pool_threads);                                        // this worker's generate
+    std::unique_ptr<Pool> enc_pool_own(o.seeder_pipeline ? new Pool(pool_threads) : nullptr);
+    Pool& enc_pool = o.seeder_pipeline ? *enc_pool_own : gen_pool;  // the encode stage's
+    struct Verified {
+      std::vector<Flood::P_ChunkKey> keys;
+      V_U64 offs;
+      V_U64 toffs;  // --gpu-encode: the text slots
+      std::string valid;
+      int arena = 0;
+    };
+    Chan<Verified> to_encode;
+    Chan<int> free_arena;
+    for (int a = 0; a < kSeedArenas; ++a) free_arena.put(a);
+    auto encode = [&](Verified& v) {
+      const std::vector<Flood::P_ChunkKey>& keys = v.keys;
+      const U8* arena = o.synthetic ? synth_mem + v.arena * synth_cap : file_arena[v.arena].data();
+      auto t1 = Clock::now();
+      // sizes and the (first-send-only) corruption decision, serially
+      std::vector<U32> sizes(keys.size(), 0);
+      std::vector<char> flip(keys.size(), 0);
+      {
+        std::lock_guard<std::mutex> g(shared_mu);
+        for (size_t k = 0; k < keys.size(); ++k) {
+          if (v.valid[k] != '1') continue;
+          sizes[k] = fl.m_runtimefiles.find(keys[k].first)->second.m_file->m_chunks[keys[k].second].m_size;
+          if (o.corrupt && sizes[k] && keys[k].second % o.corrupt == o.corrupt - 1 &&
+              corrupted.insert(keys[k]).second) {
+            flip[k] = 1;
+            ++mine.corrupted;
+          }
+        }
+      }
+      std::vector<std::string> out(keys.size());
+      enc_pool.run(keys.size(), [&](size_t k) {
+        if (v.valid[k] != '1') return;  // "send only if equal" (ChunkMethods.cpp:117-123)
+        if (o.gpu_encode) {  // the GPU's text; a wire error flips one of its characters
+          const char* t = text_mem + v.arena * text_cap + v.toffs[k];
+          const size_t tl = PeerWire::Base64PutLength(sizes[k]);
+          if (!flip[k]) {
+            out[k] = PeerWire::FrameSendChunkText(keys[k].first, keys[k].second, t, tl);
+            return;
+          }
+          std::string tmp(t, tl);
+          const size_t g = sizes[k] / 2 / 3, at = 4 * g + g / 18;  // a character of the middle byte's group
+          tmp[at] = tmp[at] == 'A' ? 'B' : 'A';
+          out[k] = PeerWire::FrameSendChunkText(keys[k].first, keys[k].second, tmp.data(), tl);
           return;
         }
-        std::string tmp(t, tl);
-        const size_t g = sizes[k] / 2 / 3, at = 4 * g + g / 18;  // a character of the middle byte's group
-        tmp[at] = tmp[at] == 'A' ? 'B' : 'A';
-        out[k] = PeerWire::FrameSendChunkText(keys[k].first, keys[k].second, tmp.data(), tl);
-        return;
-      }
-      const U8* data = arena + v.offs[k];
-      std::vector<U8> tmp;
-      if (flip[k]) {  // a wire error after the seeder's own verify
-        tmp.assign(data, data + sizes[k]);
-        tmp[sizes[k] / 2] ^= 0x01;
-        data = tmp.data();
-      }
-      out[k] = PeerWire::EncodeSendChunk(keys[k].first, keys[k].second, data, sizes[k]);
-    });
-    st.encode_s += secs(t1, Clock::now());
-    for (std::string& m : out) {
-      if (m.empty()) {
-        ++st.refused;
-        continue;
-      }
-      ++st.sent;
-      outbox.put(std::move(m));
-    }
-  };
-  std::thread encoder;
-  if (o.seeder_pipeline)
-    encoder = std::thread([&] {
-      std::vector<Verified> vs;
-      while (to_encode.take(vs, 1)) {
-        encode(vs[0]);
-        free_arena.put(vs[0].arena);
-      }
-    });
-  std::vector<Flood::P_ChunkKey> keys;
-  std::vector<int> ar;
-  while (requests.take(keys, o.batch)) {
-    st.requests += keys.size();
-    if (!free_arena.take(ar, 1)) break;
-    Verified v;
-    v.arena = ar[0];
-    auto t0 = Clock::now();
-    if (o.synthetic) {
-      // the requested chunks from the generator, 16-byte aligned in the arena,
-      // then the same GPU re-verify before sending (ChunkMethods.cpp:116-123)
-      U8* arena = synth_mem + v.arena * synth_cap;
-      std::vector<Flood::ChunkArrival> chunks(keys.size());
-      v.offs.assign(keys.size(), 0);
-      U64 total = 0;
-      for (size_t k = 0; k < keys.size(); ++k) {
-        auto it = fl.m_runtimefiles.find(keys[k].first);
-        U32 sz = 0;
-        if (it != fl.m_runtimefiles.end() && keys[k].second < it->second.m_file->m_chunks.size())
-          sz = it->second.m_file->m_chunks[keys[k].second].m_size;
-        v.offs[k] = total;
-        chunks[k] = Flood::ChunkArrival{keys[k].first, keys[k].second, total, sz};
-        total += (sz + 15) & ~15ull;
-      }
-      if (total > synth_cap) die("seeder: batch larger than its arena");
-      gen_pool.run(keys.size(), [&](size_t k) {
-        auto it = fl.m_runtimefiles.find(keys[k].first);
-        if (chunks[k].m_size == 0 || it == fl.m_runtimefiles.end()) return;
-        synth_bytes(arena + v.offs[k], it->second.m_chunkoffsets[keys[k].second], chunks[k].m_size);
+        const U8* data = arena + v.offs[k];
+        std::vector<U8> tmp;
+        if (flip[k]) {  // a wire error after the seeder's own verify
+          tmp.assign(data, data + sizes[k]);
+          tmp[sizes[k] / 2] ^= 0x01;
+          data = tmp.data();
+        }
+        out[k] = PeerWire::EncodeSendChunk(keys[k].first, keys[k].second, data, sizes[k]);
       });
-      if (o.gpu_encode) {
-        v.toffs.resize(keys.size());
-        for (size_t k = 0; k < keys.size(); ++k) v.toffs[k] = k * text_slot;
-        if (fl.VerifyEncodeChunks(arena, synth_cap, chunks, v.valid, text_mem + v.arena * text_cap, text_cap,
-                                  v.toffs) != Error::NO_ERROR_LBF)
-          die("seeder: verify + encode failed: " + std::string(Encoder::LastError()));
-      } else if (fl.VerifyChunks(arena, synth_cap, chunks, v.valid) != Error::NO_ERROR_LBF) {
+      mine.encode_s += secs(t1, Clock::now());
+      for (std::string& m : out) {
+        if (m.empty()) {
+          ++mine.refused;
+          continue;
+        }
+        ++mine.sent;
+        outbox.put(std::move(m));
+      }
+    };
+    std::thread encoder;
+    if (o.seeder_pipeline)
+      encoder = std::thread([&] {
+        std::vector<Verified> vs;
+        while (to_encode.take(vs, 1)) {
+          encode(vs[0]);
+          free_arena.put(vs[0].arena);
+        }
+      });
+    std::vector<Flood::P_ChunkKey> keys;
+    std::vector<int> ar;
+    while (requests.take(keys, o.batch)) {
+      mine.requests += keys.size();
+      if (!free_arena.take(ar, 1)) break;
+      Verified v;
+      v.arena = ar[0];
+      auto t0 = Clock::now();
+      if (o.synthetic) {
+        // the requested chunks from the generator, 16-byte aligned in the arena,
+        // then the same GPU re-verify before sending (ChunkMethods.cpp:116-123)
+        U8* arena = synth_mem + v.arena * synth_cap;
+        std::vector<Flood::ChunkArrival> chunks(keys.size());
+        v.offs.assign(keys.size(), 0);
+        U64 total = 0;
+        for (size_t k = 0; k < keys.size(); ++k) {
+          auto it = fl.m_runtimefiles.find(keys[k].first);
+          U32 sz = 0;
+          if (it != fl.m_runtimefiles.end() && keys[k].second < it->second.m_file->m_chunks.size())
+            sz = it->second.m_file->m_chunks[keys[k].second].m_size;
+          v.offs[k] = total;
+          chunks[k] = Flood::ChunkArrival{keys[k].first, keys[k].second, total, sz};
+          total += (sz + 15) & ~15ull;
+        }
+        if (total > synth_cap) die("seeder: batch larger than its arena");
+        gen_pool.run(keys.size(), [&](size_t k) {
+          auto it = fl.m_runtimefiles.find(keys[k].first);
+          if (chunks[k].m_size == 0 || it == fl.m_runtimefiles.end()) return;
+          synth_bytes(arena + v.offs[k], it->second.m_chunkoffsets[keys[k].second], chunks[k].m_size);
+        });
+        if (o.gpu_encode) {
+          v.toffs.resize(keys.size());
+          for (size_t k = 0; k < keys.size(); ++k) v.toffs[k] = k * text_slot;
+          if (fl.VerifyEncodeChunks(arena, synth_cap, chunks, v.valid, text_mem + v.arena * text_cap, text_cap,
+                                    v.toffs) != Error::NO_ERROR_LBF)
+            die("seeder: verify + encode failed: " + std::string(Encoder::LastError()));
+        } else if (fl.VerifyChunks(arena, synth_cap, chunks, v.valid) != Error::NO_ERROR_LBF) {
+          die("seeder: verify failed: " + std::string(Encoder::LastError()));
+        }
+      } else if (fl.ReadVerifiedChunks(keys, file_arena[v.arena], v.offs, v.valid) != Error::NO_ERROR_LBF) {
         die("seeder: verify failed: " + std::string(Encoder::LastError()));
       }
-    } else if (fl.ReadVerifiedChunks(keys, file_arena[v.arena], v.offs, v.valid) != Error::NO_ERROR_LBF) {
-      die("seeder: verify failed: " + std::string(Encoder::LastError()));
+      mine.verify_s += secs(t0, Clock::now());
+      v.keys = std::move(keys);
+      keys = std::vector<Flood::P_ChunkKey>();
+      if (o.seeder_pipeline) {
+        to_encode.put(std::move(v));
+      } else {
+        encode(v);
+        free_arena.put(v.arena);
+      }
     }
-    st.verify_s += secs(t0, Clock::now());
-    v.keys = std::move(keys);
-    keys = std::vector<Flood::P_ChunkKey>();
-    if (o.seeder_pipeline) {
-      to_encode.put(std::move(v));
-    } else {
-      encode(v);
-      free_arena.put(v.arena);
+    to_encode.close();
+    if (encoder.joinable()) encoder.join();
+    if (synth_mem) {
+      for (int a = 0; a < kSeedArenas; ++a)
+        if (o.register_arenas) (void)lbf_host_unregister(ctx, synth_mem + a * synth_cap);
+      free(synth_mem);
     }
-  }
-  to_encode.close();
-  if (encoder.joinable()) encoder.join();
+    if (text_mem) {
+      for (int a = 0; a < kSeedArenas; ++a)
+        if (o.register_arenas) (void)lbf_host_unregister(ctx, text_mem + a * text_cap);
+      free(text_mem);
+    }
+    std::lock_guard<std::mutex> g(shared_mu);
+    st.requests += mine.requests;
+    st.sent += mine.sent;
+    st.refused += mine.refused;
+    st.corrupted += mine.corrupted;
+    st.verify_s += mine.verify_s;
+    st.encode_s += mine.encode_s;
+  };
+  std::vector<std::thread> others;
+  for (unsigned w = 1; w < o.seeder_workers; ++w) others.emplace_back(worker, w);
+  worker(0);
+  for (std::thread& t : others) t.join();
   outbox.close();
   sender.join();
   reader.join();
   close(fd);
-  if (synth_mem) {
-    for (int a = 0; a < kSeedArenas; ++a)
-      if (o.register_arenas) (void)lbf_host_unregister(ctx, synth_mem + a * synth_cap);
-    free(synth_mem);
-  }
-  if (text_mem) {
-    for (int a = 0; a < kSeedArenas; ++a)
-      if (o.register_arenas) (void)lbf_host_unregister(ctx, text_mem + a * text_cap);
-    free(text_mem);
-  }
-  lbf_ctx_destroy(ctx);
+  for (lbf_ctx* c : wctx) lbf_ctx_destroy(c);
 }
 
 // ---- leecher -------------------------------------------------------------------
@@ -656,6 +690,7 @@ int main(int argc, char** argv) {
     else if (a == "--pipelined-seeder") o.seeder_pipeline = true;
     else if (a == "--gpu-decode") o.gpu_decode = true;
     else if (a == "--cpu-decode") o.gpu_decode = false;
+    else if (a == "--seeder-workers") o.seeder_workers = (unsigned)strtoul(val(), nullptr, 10);
     else if (a == "--gpu-encode") o.gpu_encode = true;
     else if (a == "--cpu-encode") o.gpu_encode = false;
     else {
@@ -664,12 +699,13 @@ int main(int argc, char** argv) {
               "                    [--threads T]\n"
               "                    [--corrupt K] [--dir DIR] [--keep] [--synthetic] [--no-register]\n"
               "                    [--verifiers V] [--pipelined-seeder] [--gpu-decode | --cpu-decode]\n"
-              "                    [--gpu-encode | --cpu-encode]\n");
+              "                    [--gpu-encode | --cpu-encode] [--seeder-workers S]\n");
       return 2;
     }
   }
   if (o.chunksize == 0 || o.window == 0 || o.batch == 0) die("chunksize, window and batch must be > 0");
   if (o.verifiers == 0 || o.verifiers > 8) die("verifiers must be 1..8");
+  if (o.seeder_workers == 0 || o.seeder_workers > 8) die("seeder workers must be 1..8");
   if (o.gpu_encode && !o.synthetic) die("--gpu-encode needs --synthetic (the file seeder reads and verifies in one call)");
   if (o.dir.empty()) {
     const char* t = getenv("TMPDIR");
@@ -1031,7 +1067,7 @@ int main(int argc, char** argv) {
   const double wall = secs(t_start, t_end);
   printf("{\"config\": \"C5 loopback 2-peer\", \"bytes\": %llu, \"chunk_size\": %u, \"chunks\": %zu, "
          "\"window\": %u, \"batch\": %u, \"deadline_ms\": %u, \"verifiers\": %u, \"seeder_pipelined\": %s, "
-         "\"gpu_decode\": %s, \"gpu_encode\": %s, "
+         "\"gpu_decode\": %s, \"gpu_encode\": %s, \"seeder_workers\": %u, "
          "\"threads\": %u, \"seconds\": %.3f, \"payload_gibs\": %.3f, "
          "\"wire_gibs\": %.3f, \"encode_flood_s\": %.3f, "
          "\"leecher\": {\"batches\": %zu, \"mean_batch\": %.1f, \"decode_s\": %.3f, \"verify_s\": %.3f, "
@@ -1043,7 +1079,7 @@ int main(int argc, char** argv) {
          "\"seed_source\": \"%s\", \"arenas_registered\": %s}\n",
          (unsigned long long)o.size, o.chunksize, total, o.window, o.batch, o.deadline_ms, o.verifiers,
          o.seeder_pipeline ? "true" : "false", o.gpu_decode ? "true" : "false",
-         o.gpu_encode ? "true" : "false", o.threads, wall,
+         o.gpu_encode ? "true" : "false", o.seeder_workers, o.threads, wall,
          payload / wall / (1u << 30), wire_bytes / wall / (1u << 30), encode_s, batches,
          batches ? (double)(accepted + rejected) / batches : 0.0, decode_s, verify_s, write_s, rejected, undecodable,
          (unsigned long long)sst.requests, (unsigned long long)sst.sent, (unsigned long long)sst.refused, sst.verify_s,

@@ -138,6 +138,9 @@ def test_loopback_two_peers(tmp_path, size, cs, window, batch, corrupt, syntheti
     (["--verifiers", "1"], False),
     (["--verifiers", "2", "--gpu-encode"], True),                          # the seeder's encode on the GPU too
     (["--verifiers", "1", "--gpu-encode", "--pipelined-seeder", "--cpu-decode"], True),
+    (["--verifiers", "2", "--seeder-workers", "2"], True),                # two seeder workers, each its own context
+    (["--verifiers", "2", "--seeder-workers", "3", "--pipelined-seeder"], False),
+    (["--verifiers", "2", "--seeder-workers", "2", "--gpu-encode"], True),
 ])
 def test_loopback_verifier_counts(tmp_path, extra, synthetic):
     """The leecher's verifiers (each with its own GPU context and a copy of the
@@ -149,6 +152,7 @@ def test_loopback_verifier_counts(tmp_path, extra, synthetic):
     assert r["verifiers"] == int(extra[1]) and r["seeder_pipelined"] is ("--pipelined-seeder" in extra)
     assert r["gpu_decode"] is ("--cpu-decode" not in extra)
     assert r["gpu_encode"] is ("--gpu-encode" in extra)
+    assert r["seeder_workers"] == (int(extra[extra.index("--seeder-workers") + 1]) if "--seeder-workers" in extra else 1)
 
 
 @pytest.mark.gpu

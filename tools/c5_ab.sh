@@ -7,7 +7,8 @@
 # verifier, pipelined seeder; v2 = two verifiers, pipelined seeder; v2s = two
 # verifiers, serial seeder; gd = v2s with the leecher's base64 decode on the
 # GPU (the default since round 4); gd1 = gd with one verifier; ge = gd with
-# the seeder's base64 encode on the GPU too (--gpu-encode);
+# the seeder's base64 encode on the GPU too (--gpu-encode); sw2 = gd with two
+# seeder workers; sw2e = sw2 with --gpu-encode; sw3 = gd with three seeder workers;
 # pre = v2s run by bitflood_amd/lib/lbf_loopback_prepool when that binary exists
 # (a build of an earlier lbf_loopback.cpp, for an A/B across a harness change).
 set -o pipefail
@@ -20,7 +21,9 @@ export TMPDIR=${TMPDIR:-/tmp}
 declare -A flags=([r03]="--verifiers 1 --cpu-decode" [v1]="--verifiers 1 --pipelined-seeder --cpu-decode" \
                   [v2]="--verifiers 2 --pipelined-seeder --cpu-decode" [v2s]="--verifiers 2 --cpu-decode" \
                   [gd]="--verifiers 2 --gpu-decode" [gd1]="--verifiers 1 --gpu-decode" \
-                  [ge]="--verifiers 2 --gpu-decode --gpu-encode" [pre]="--verifiers 2")
+                  [ge]="--verifiers 2 --gpu-decode --gpu-encode" \
+                  [sw2]="--verifiers 2 --seeder-workers 2" [sw2e]="--verifiers 2 --seeder-workers 2 --gpu-encode" \
+                  [sw3]="--verifiers 2 --seeder-workers 3" [pre]="--verifiers 2")
 for r in $(seq "$rounds"); do
   for v in $variants; do
     bin=bitflood_amd/lib/lbf_loopback
