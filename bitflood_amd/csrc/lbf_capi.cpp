@@ -1653,7 +1653,8 @@ extern "C" int lbf_verify_encode_b64_batch(lbf_ctx* ctx, const uint8_t* data, ui
     tlo = std::min(tlo, text_offsets[i]);
     thi = std::max(thi, text_offsets[i] + tl);
   }
-  dlo &= ~15ull;  // device offsets keep the host offsets' alignment mod 16
+  const uint64_t text_first = tlo;  // the D2H starts here: no byte before the lowest slot is written
+  dlo &= ~15ull;                    // device offsets keep the host offsets' alignment mod 16
   tlo &= ~15ull;
   return guarded([&] {
     auto up = [](uint64_t x, uint64_t a) { return (x + a - 1) / a * a; };
@@ -1689,7 +1690,9 @@ extern "C" int lbf_verify_encode_b64_batch(lbf_ctx* ctx, const uint8_t* data, ui
     if (int rc = lbf_sha1_launch(d_data, d_doff, d_sz, n, nullptr, d_exp, d_ver, st)) return rc;
     if (int rc = lbf::launch_b64_encode(d_data, d_doff, d_sz, d_text, d_toff, (uint32_t)n, st)) return rc;
     LBF_HIP_TRY(hipMemcpyAsync(verdicts, d_ver, n, hipMemcpyDeviceToHost, st));
-    if (thi > tlo) LBF_HIP_TRY(hipMemcpyAsync(text + tlo, d_text, thi - tlo, hipMemcpyDeviceToHost, st));
+    if (thi > text_first)
+      LBF_HIP_TRY(hipMemcpyAsync(text + text_first, d_text + (text_first - tlo), thi - text_first, hipMemcpyDeviceToHost,
+                                 st));
     LBF_HIP_TRY(hipStreamSynchronize(st));
     return (int)LBF_OK;
   });
@@ -1723,7 +1726,9 @@ extern "C" int lbf_b64_verify_batch(lbf_ctx* ctx, const char* text, uint64_t tex
       ohi = std::max(ohi, out_offsets[i] + expected_sizes[i]);
     }
   }
-  // device offsets keep the host offsets' alignment mod 16
+  // device offsets keep the host offsets' alignment mod 16; the D2H starts at
+  // the lowest slot itself (out_first), so no byte before it is written
+  const uint64_t out_first = olo;
   tlo &= ~15ull;
   if (out) olo &= ~15ull;
   return guarded([&] {
@@ -1789,7 +1794,8 @@ extern "C" int lbf_b64_verify_batch(lbf_ctx* ctx, const char* text, uint64_t tex
     if (int rc = lbf_sha1_launch(d_out, d_ooff, d_sizes, n, nullptr, d_exp, d_ver, st)) return rc;
     std::vector<uint8_t> res(n * 6);
     LBF_HIP_TRY(hipMemcpyAsync(res.data(), d_res, res.size(), hipMemcpyDeviceToHost, st));
-    if (out && ohi > olo) LBF_HIP_TRY(hipMemcpyAsync(out + olo, d_out, ohi - olo, hipMemcpyDeviceToHost, st));
+    if (out && ohi > out_first)
+      LBF_HIP_TRY(hipMemcpyAsync(out + out_first, d_out + (out_first - olo), ohi - out_first, hipMemcpyDeviceToHost, st));
     LBF_HIP_TRY(hipStreamSynchronize(st));
     const uint32_t* sizes = reinterpret_cast<const uint32_t*>(res.data());
     const uint8_t* over = res.data() + 4 * n;

@@ -200,3 +200,45 @@ def test_sender_encode_matches_xmlrpc_text(hasher):
     # round trip through the receiver's device decode
     rv, rs, out, ooff, _ = _batch(hasher, texts, datas)
     assert rv.all() and list(rs) == sizes
+
+
+def test_outputs_touch_nothing_outside_their_slots(hasher):
+    """Both entry points copy results back from the lowest slot on: the bytes
+    of `out` / `text` before the first slot and after the last stay as they
+    were, whatever the slots' alignment (the device copies keep it mod 16)."""
+    rng = np.random.default_rng(3)
+    datas = [rng.integers(0, 256, n, dtype=np.uint8).tobytes() for n in (1000, 77, 4099)]
+    exp = np.frombuffer(b"".join(hashlib.sha1(d).digest() for d in datas), dtype=np.uint8).reshape(-1, 20)
+    texts = [xmlrpc_text(d) for d in datas]
+    for first in (5, 16, 27):
+        # decode: out slots from `first` on, sentinel everywhere else
+        ooff = np.array([first, first + 1100, first + 1200], dtype=np.uint64)
+        out = np.full(first + 1200 + 4099 + 40, 0xAB, dtype=np.uint8)
+        toffs, pos, buf = [], 3, bytearray(b"\0" * 3)
+        for t in texts:
+            toffs.append(pos)
+            buf += t
+            pos += len(t)
+        text = np.frombuffer(bytes(buf), dtype=np.uint8)
+        esz = [len(d) for d in datas]
+        ver, dec = hasher.verify_b64(text, toffs, [len(t) for t in texts], esz, exp, out, ooff)
+        assert ver.all()
+        assert (out[:first] == 0xAB).all() and (out[first + 1200 + 4099:] == 0xAB).all()
+        for i, d in enumerate(datas):
+            assert out[int(ooff[i]):int(ooff[i]) + len(d)].tobytes() == d
+        # encode: text slots from `first` on
+        lens = [len(t) for t in texts]
+        tslot = np.array([first, first + lens[0] + 9, first + lens[0] + lens[1] + 20], dtype=np.uint64)
+        tbuf = np.full(int(tslot[-1]) + lens[2] + 40, 0xCD, dtype=np.uint8)
+        data = np.frombuffer(b"".join(datas), dtype=np.uint8)
+        offs = np.array([0, 1000, 1077], dtype=np.uint64)
+        sz = np.array(esz, dtype=np.uint32)
+        v = np.zeros(3, dtype=np.uint8)
+        e = np.ascontiguousarray(exp)
+        assert hasher._lib.lbf_verify_encode_b64_batch(hasher._h, data.ctypes.data, data.size, offs.ctypes.data,
+                                                       sz.ctypes.data, 3, e.ctypes.data, v.ctypes.data,
+                                                       tbuf.ctypes.data, tbuf.size, tslot.ctypes.data) == 0
+        assert v.all()
+        assert (tbuf[:first] == 0xCD).all() and (tbuf[int(tslot[-1]) + lens[2]:] == 0xCD).all()
+        for i, t in enumerate(texts):
+            assert tbuf[int(tslot[i]):int(tslot[i]) + len(t)].tobytes() == t
