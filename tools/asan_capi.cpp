@@ -7,6 +7,8 @@
 //   lbf_sha1_batch / lbf_verify_batch (host memory) and
 //   lbf_file_ranges (hash and verify, including a truncated file) and
 //   lbf_files_ranges (verify over 2-4 truncated or missing files)
+//   lbf_verify_encode_b64_batch + lbf_b64_verify_batch (the wire form both ways:
+//   text slots at ragged offsets, some texts cut short)
 // against the oracle (oracle/sha1_oracle.c, compiled in as the checker).  Half
 // the jobs read from memory registered with the context, and half the
 // contexts then take three concurrent callers with 24-40 MiB batches (enough
@@ -186,6 +188,52 @@ int main(int argc, char** argv) {
         CHECK(mver[i] == (present ? 1 : 0), "files verdict %lu (file %u)", (unsigned long)i, f);
       }
       for (uint32_t f = 0; f < nf; ++f) unlink(fpaths[f].c_str());
+      // the wire form both ways: encode (with the corrupted digests above) into
+      // text slots at ragged offsets between sentinels, then decode the texts
+      // back, some cut short, against the true digests
+      {
+        const uint64_t m = std::min<uint64_t>(n, 200);
+        std::vector<uint64_t> toff(m), ooff(m);
+        std::vector<uint32_t> tlen(m), dlen(m), dsz(m, 0);
+        uint64_t tpos = uni(0, 40), opos = uni(0, 40);
+        for (uint64_t i = 0; i < m; ++i) {
+          toff[i] = tpos;
+          tlen[i] = (uint32_t)lbf_b64_put_length(size[i]);
+          tpos += tlen[i] + uni(0, 40);
+          ooff[i] = opos;
+          opos += size[i] + uni(0, 40);
+        }
+        const uint64_t thead = m ? toff[0] : 0, ohead = m ? ooff[0] : 0;
+        const uint64_t ttail = m ? toff[m - 1] + tlen[m - 1] : 0, otail = m ? ooff[m - 1] + size[m - 1] : 0;
+        std::vector<char> text(tpos + 64, '\x01');
+        std::vector<uint8_t> ev(m, 7), dv(m, 7), cut(m, 0), out(opos + 64, 0xA5);
+        rc = lbf_verify_encode_b64_batch(ctx, buf.data(), buf_len, off.data(), size.data(), m, exp.data(), ev.data(),
+                                         text.data(), text.size(), toff.data());
+        CHECK(rc == LBF_OK, "encode rc %d: %s", rc, lbf_last_error());
+        for (uint64_t i = 0; i < m && rc == LBF_OK; ++i) CHECK(ev[i] == (bad[i] ? 0 : 1), "encode verdict %lu", (unsigned long)i);
+        for (uint64_t k = 0; k < thead; ++k) CHECK(text[k] == '\x01', "text byte %lu before the first slot", (unsigned long)k);
+        for (uint64_t k = ttail; k < text.size(); ++k) CHECK(text[k] == '\x01', "text byte %lu after the last slot", (unsigned long)k);
+        for (uint64_t i = 0; i < m; ++i) {
+          dlen[i] = tlen[i];
+          if (tlen[i] >= 8 && uni(0, 5) == 0) {  // lose at least one group
+            dlen[i] = (uint32_t)uni(0, tlen[i] - 4);
+            cut[i] = 1;
+          }
+        }
+        rc = lbf_b64_verify_batch(ctx, text.data(), text.size(), toff.data(), dlen.data(), m, size.data(), want.data(),
+                                  out.data(), out.size(), ooff.data(), dsz.data(), dv.data());
+        CHECK(rc == LBF_OK, "decode rc %d: %s", rc, lbf_last_error());
+        for (uint64_t i = 0; i < m && rc == LBF_OK; ++i) {
+          CHECK(dv[i] == (cut[i] ? 0 : 1), "decode verdict %lu (cut %d)", (unsigned long)i, cut[i]);
+          CHECK(cut[i] ? dsz[i] < size[i] : dsz[i] == size[i], "decoded size %lu: %u of %u", (unsigned long)i, dsz[i],
+                size[i]);
+          if (!cut[i])
+            CHECK(memcmp(out.data() + ooff[i], buf.data() + off[i], size[i]) == 0, "decoded bytes %lu", (unsigned long)i);
+        }
+        for (uint64_t k = 0; k < ohead; ++k) CHECK(out[k] == 0xA5, "out byte %lu before the first slot", (unsigned long)k);
+        for (uint64_t k = otail; k < out.size(); ++k) CHECK(out[k] == 0xA5, "out byte %lu after the last slot", (unsigned long)k);
+        chunks_checked += (long)(2 * m);
+      }
     }
     if (uni(0, 1) == 0) {
       // three concurrent callers on this context (calls serialize on its
