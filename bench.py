@@ -261,7 +261,15 @@ def dist_setup(args):
     dev = local % ndev
     torch.cuda.set_device(dev)
     if world > 1 or os.environ.get("LBF_BENCH_FORM_GROUP") == "1":
-        init_group(os.environ.get("LBF_BENCH_BACKEND", "nccl"), rank, world, dev)
+        backend = os.environ.get("LBF_BENCH_BACKEND")
+        if backend is None:
+            # the self-launch's rule under an outside launcher too: RCCL refuses
+            # two ranks on one device, so more ranks than GPUs rehearse on gloo
+            backend = "gloo" if world > ndev else "nccl"
+            if backend == "gloo" and rank == 0:
+                print(f"bench.py: {world} ranks on {ndev} visible GPU(s): process group gloo (rehearsal)",
+                      file=sys.stderr)
+        init_group(backend, rank, world, dev)
     return rank, world, local, dev, ndev
 
 

@@ -173,3 +173,21 @@ def test_self_launch_refused_under_a_profiler():
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], env=env, capture_output=True,
                        text=True, timeout=120, cwd=ROOT)
     assert p.returncode != 0 and "not allowed under rocprofv3" in p.stderr, (p.returncode, p.stderr[-2000:])
+
+
+def test_outside_launcher_with_more_ranks_than_gpus_uses_gloo():
+    """Under torch.distributed.run the bench picks the process group by the
+    self-launch's rule: RCCL refuses two ranks on one device, so with more
+    ranks than visible GPUs (here none) and no LBF_BENCH_BACKEND it forms a gloo
+    group instead of failing in init_process_group."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LBF_BENCH_BACKEND")}
+    port = str(bench._free_port())
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", port, FAKE, "--gpus", "2"] + FAKE_ARGV,
+                       env=env, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    out = json.loads([x for x in p.stdout.splitlines() if x.strip().startswith("{")][-1])
+    _check_line(out, 2)
+    assert out["ranks"]["process_group"] == "gloo"
+    assert "process group gloo (rehearsal)" in p.stderr
