@@ -543,8 +543,9 @@ def e2e_leg(host_data, cs, dev, world):
 
 
 def inproc_leg(buf, slice_bytes, cs, shard_starts, slice_hashes):
-    """EncodeFile's shape on an N-GPU node: ONE process, ONE lbf_ctx over every
-    visible device, lbf_sha1_batch on one N x slice_bytes host buffer (slice r
+    """EncodeFile's shape on an N-GPU node: ONE process, ONE lbf_ctx over the
+    run's N devices (the first N visible; all of them on a rehearsal with fewer
+    GPUs than ranks), lbf_sha1_batch on one N x slice_bytes host buffer (slice r
     = the bytes rank r hashed in its e2e leg), registered, then pageable.  Run
     by rank 0 after the other ranks have finished.  `buf` (a device buffer of
     at least slice_bytes) generates each slice; parity: slice r's digests must
@@ -570,7 +571,9 @@ def inproc_leg(buf, slice_bytes, cs, shard_starts, slice_hashes):
             t = min(t, time.perf_counter() - t0)
         return gib / t, d
 
-    with ChunkHasher(device_mask=0) as h:
+    # the N GPUs the ranks ran on, not every GPU the node has (N=2 on an 8-GPU node)
+    use = min(world, max(1, torch.cuda.device_count()))
+    with ChunkHasher(device_mask=(1 << use) - 1) as h:
         info = [h.worker_info(w) for w in range(h.num_workers)]
         ndev = h.num_devices
         h.hash_chunks(big, offs, sizes)  # warm: every worker's staging and device slots
@@ -586,7 +589,7 @@ def inproc_leg(buf, slice_bytes, cs, shard_starts, slice_hashes):
     del big
     ok = [int(slice_hash(d_reg[r * per_slice:(r + 1) * per_slice]) == slice_hashes[r]) for r in range(world)]
     return {
-        "what": "one process, one lbf_ctx over every visible device, lbf_sha1_batch on one host buffer of "
+        "what": f"one process, one lbf_ctx over {use} device(s), lbf_sha1_batch on one host buffer of "
                 f"{world} x {slice_bytes / GIB:g} GiB (slice r = rank r's e2e bytes)",
         "devices": ndev, "workers": len(info), "workers_per_device": int(os.environ.get("LBF_WORKERS_PER_DEVICE", "1")),
         "bytes": total, "chunk_size": cs,
