@@ -9,6 +9,7 @@
 # GPU (the default since round 4); gd1 = gd with one verifier; ge = gd with
 # the seeder's base64 encode on the GPU too (--gpu-encode); sw2 = gd with two
 # seeder workers; sw2e = sw2 with --gpu-encode; sw3 = gd with three seeder workers;
+# gd3 / gd4 = gd with three / four leecher verifiers;
 # pre = v2s run by bitflood_amd/lib/lbf_loopback_prepool when that binary exists
 # (a build of an earlier lbf_loopback.cpp, for an A/B across a harness change).
 set -o pipefail
@@ -23,7 +24,8 @@ declare -A flags=([r03]="--verifiers 1 --cpu-decode" [v1]="--verifiers 1 --pipel
                   [gd]="--verifiers 2 --gpu-decode" [gd1]="--verifiers 1 --gpu-decode" \
                   [ge]="--verifiers 2 --gpu-decode --gpu-encode" \
                   [sw2]="--verifiers 2 --seeder-workers 2" [sw2e]="--verifiers 2 --seeder-workers 2 --gpu-encode" \
-                  [sw3]="--verifiers 2 --seeder-workers 3" [pre]="--verifiers 2")
+                  [sw3]="--verifiers 2 --seeder-workers 3" \
+                  [gd3]="--verifiers 3" [gd4]="--verifiers 4" [pre]="--verifiers 2")
 for r in $(seq "$rounds"); do
   for v in $variants; do
     bin=bitflood_amd/lib/lbf_loopback
