@@ -1750,9 +1750,10 @@ extern "C" int lbf_b64_verify_batch(lbf_ctx* ctx, const char* text, uint64_t tex
       }
     }
     if (out) outb = ohi - olo;
-    // device layout: text | sextets | bytes | inputs (offsets, lengths, caps, expected) | outputs (sizes, over, verdicts)
+    // device layout: text | sextets | bytes | inputs (offsets, lengths, caps, expected, zeroed redo flags) |
+    // outputs (sizes, over, verdicts)
     const uint64_t text_b = up(thi - tlo, 256), sext_b = up(sext, 256), out_b = up(outb + 16, 256);
-    const uint64_t in_b = up(n * (8 * 3 + 4 * 2 + 20), 256), res_b = up(n * (4 + 1 + 1), 256);
+    const uint64_t in_b = up(n * (8 * 3 + 4 * 2 + 20 + 1), 256), res_b = up(n * (4 + 1 + 1), 256);
     const uint64_t need = text_b + sext_b + out_b + in_b + res_b;
     std::lock_guard<std::mutex> lock(ctx->mu);
     KeepCurrentDevice keep;
@@ -1764,7 +1765,7 @@ extern "C" int lbf_b64_verify_batch(lbf_ctx* ctx, const char* text, uint64_t tex
     uint8_t* d_out = d_sext + sext_b;
     uint8_t* d_in = d_out + out_b;
     uint8_t* d_res = d_in + in_b;
-    std::vector<uint8_t> in(n * (8 * 3 + 4 * 2 + 20));
+    std::vector<uint8_t> in(n * (8 * 3 + 4 * 2 + 20 + 1), 0);
     uint8_t* q = in.data();
     auto put = [&](const void* src, uint64_t bytes) {
       memcpy(q, src, bytes);
@@ -1785,10 +1786,11 @@ extern "C" int lbf_b64_verify_batch(lbf_ctx* ctx, const char* text, uint64_t tex
     const uint32_t* d_tlen = reinterpret_cast<const uint32_t*>(d_ooff + n);
     const uint32_t* d_cap = d_tlen + n;
     const uint8_t* d_exp = reinterpret_cast<const uint8_t*>(d_cap + n);
+    uint8_t* d_redo = const_cast<uint8_t*>(d_exp) + 20 * n;  // uploaded as zeros
     uint32_t* d_sizes = reinterpret_cast<uint32_t*>(d_res);
     uint8_t* d_over = reinterpret_cast<uint8_t*>(d_sizes + n);
     uint8_t* d_ver = d_over + n;
-    lbf::B64Launch b{d_text, d_sext, d_toff, d_soff, d_tlen, d_out, d_ooff, d_cap, d_sizes, d_over, (uint32_t)n};
+    lbf::B64Launch b{d_text, d_sext, d_toff, d_soff, d_tlen, d_out, d_ooff, d_cap, d_sizes, d_over, d_redo, (uint32_t)n};
     if (int rc = lbf::launch_b64_decode(b, st)) return rc;
     // the decoded lengths are the chunk sizes the hash kernels read
     if (int rc = lbf_sha1_launch(d_out, d_ooff, d_sizes, n, nullptr, d_exp, d_ver, st)) return rc;

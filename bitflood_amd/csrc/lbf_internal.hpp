@@ -50,6 +50,7 @@ struct B64Launch {
   const uint32_t* cap;
   uint32_t* sizes;
   uint8_t* over;
+  uint8_t* redo;  // n bytes, zero on entry: the chunks the one-pass decode hands to the general one
   uint32_t n;
 };
 int launch_b64_decode(const B64Launch& b, hipStream_t stream);

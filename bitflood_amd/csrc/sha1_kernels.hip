@@ -181,8 +181,15 @@ int launch_chunks(const ChunkParams& p, hipStream_t stream) {
 
 int launch_b64_decode(const B64Launch& b, hipStream_t stream) {
   if (b.n == 0) return LBF_OK;
+  // the one-pass decode of canonically laid-out text, split over enough
+  // workgroups to fill the chip at small batches; then the general two-pass
+  // decode of whatever it handed back (a workgroup per chunk, most exit at once)
+  const uint32_t parts = std::max(1u, std::min(16u, 2048u / b.n));
+  hipLaunchKernelGGL(b64_decode_canon_kernel, dim3(b.n, parts), dim3(kB64Threads), 0, stream, b.text, b.text_off,
+                     b.text_len, b.out, b.out_off, b.cap, b.sizes, b.over, b.redo);
+  LBF_HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL(b64_decode_kernel, dim3(b.n), dim3(kB64Threads), 0, stream, b.text, b.scratch, b.text_off,
-                     b.sext_off, b.text_len, b.out, b.out_off, b.cap, b.sizes, b.over);
+                     b.sext_off, b.text_len, b.out, b.out_off, b.cap, b.sizes, b.over, (const uint8_t*)b.redo);
   LBF_HIP_TRY(hipGetLastError());
   return LBF_OK;
 }

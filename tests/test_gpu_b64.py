@@ -109,17 +109,19 @@ def test_well_formed_frames_every_size(hasher, align, shift):
 
 
 def test_perturbed_texts_match_the_reference_decoder(hasher):
-    """Junk characters anywhere, '=' anywhere, characters dropped, truncation:
-    the device's bytes and lengths equal b64get's, and a verdict is 1 exactly
-    when the decoded bytes are the original chunk."""
+    """Junk characters anywhere, '=' anywhere, characters dropped, truncation,
+    and replacements that keep the encoder's length ('=', junk or an alphabet
+    character in place of another, so the one-pass decode reads them and must
+    hand the chunk back): the device's bytes and lengths equal b64get's, and a
+    verdict is 1 exactly when the decoded bytes are the original chunk."""
     rng = np.random.default_rng(5)
     junk = [c for c in range(256) if _DEC[c] == SKIP]
     texts, datas, wants = [], [], []
-    for case in range(400):
+    for case in range(540):
         n = int(rng.integers(0, 3000))
         d = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
         t = bytearray(xmlrpc_text(d))
-        kind = case % 6
+        kind = case % 9
         if kind == 1 and t:  # junk inserted
             for _ in range(int(rng.integers(1, 20))):
                 t.insert(int(rng.integers(0, len(t) + 1)), int(rng.choice(junk)))
@@ -135,6 +137,13 @@ def test_perturbed_texts_match_the_reference_decoder(hasher):
             j = int(rng.integers(0, len(t)))
             if _DEC[t[j]] < 64:
                 t[j] = b"A"[0] if t[j] != b"A"[0] else b"B"[0]
+        elif kind == 6 and len(t) > 4:  # '=' in place of a character before the last group
+            t[int(rng.integers(0, len(t) - 4))] = ord("=")
+        elif kind == 7 and t:  # junk in place of a character
+            t[int(rng.integers(0, len(t)))] = int(rng.choice(junk))
+        elif kind == 8 and b" " in t:  # an alphabet character in place of a separator
+            seps = [j for j, c in enumerate(t) if c == ord(" ")]
+            t[seps[int(rng.integers(0, len(seps)))]] = ord("Q")
         texts.append(bytes(t))
         datas.append(d)
         wants.append(b64get(bytes(t)))
