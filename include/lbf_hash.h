@@ -178,8 +178,9 @@ int lbf_b64_verify_batch(lbf_ctx* ctx, const char* text, uint64_t text_len, cons
  * its text -- four characters per three bytes, a space (the frame's newline)
  * after every 18th complete group, "xx==" / "xxx=" for a last one or two
  * bytes -- lands at text[text_offsets[i], + lbf_b64_put_length(sizes[i]))
- * whatever the verdict.  Bytes of `text` between the lowest slot and the end
- * of the highest that are not written text are unspecified afterwards.
+ * whatever the verdict (slots must not overlap).  Bytes of `text` between the
+ * lowest slot and the end of the highest that are not written text are
+ * unspecified afterwards; bytes outside that span are not written.
  * Synchronous, on the context's first device. */
 int lbf_verify_encode_b64_batch(lbf_ctx* ctx, const uint8_t* data, uint64_t data_len, const uint64_t* offsets,
                                 const uint32_t* sizes, uint64_t n, const uint8_t* expected, uint8_t* verdicts,
