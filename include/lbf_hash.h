@@ -162,7 +162,8 @@ int lbf_files_ranges(lbf_ctx* ctx, const char* const* paths, uint32_t n_files, c
  * non-NULL the decoded bytes land at out[out_offsets[i], + expected_sizes[i])
  * (host memory, slots must not overlap); bytes of `out` between the lowest
  * slot and the end of the highest that are not decoded bytes are unspecified
- * afterwards.  Synchronous, on the context's first device.  Text and output
+ * afterwards; bytes outside that span are not written.  Synchronous, on the
+ * context's first device.  Text and output
  * in memory registered with lbf_host_register move by DMA without staging. */
 int lbf_b64_verify_batch(lbf_ctx* ctx, const char* text, uint64_t text_len, const uint64_t* text_offsets,
                          const uint32_t* text_lens, uint64_t n, const uint32_t* expected_sizes,
