@@ -62,12 +62,36 @@ DEFINE_KERNEL(k_bfi, OP_BFI)
 DEFINE_KERNEL(k_bitop3, OP_BITOP3)
 DEFINE_KERNEL(k_perm, OP_PERM)
 DEFINE_KERNEL(k_lshladd, OP_LSHLADD)
+#define OP_MIX_AX(x) OP_ALIGN(x) OP_XOR(x)
+#define OP_MIX_A3A(x) OP_ADD3(x) OP_ADD(x)
+#define OP_MIX_AB(x) OP_ALIGN(x) OP_BITOP3X(x)
+#define HALF8(OP) OP(a0) OP(a1) OP(a2) OP(a3) OP(a4) OP(a5) OP(a6) OP(a7)
+// 32 instructions per iteration like the others: 16 slow + 16 fast, interleaved
+#define DEFINE_MIX(NAME, PAIR)                                                               \
+  __global__ void __launch_bounds__(256) NAME(uint32_t iters, uint32_t* out, unsigned long long* clk) { \
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime(); \
+    uint32_t a0 = threadIdx.x, a1 = a0 * 3, a2 = a0 * 5, a3 = a0 * 7, a4 = a0 * 11,         \
+             a5 = a0 * 13, a6 = a0 * 17, a7 = a0 * 19;                                      \
+    const uint32_t b = blockIdx.x | 1, c = blockIdx.x * 7 + 3;                               \
+    for (uint32_t i = 0; i < iters; ++i) {                                                   \
+      HALF8(PAIR) HALF8(PAIR)                                                                \
+    }                                                                                        \
+    out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;    \
+    if (blockIdx.x == 0 && threadIdx.x == 0) {                                               \
+      clk[0] = __builtin_amdgcn_s_memtime() - t0;                                            \
+      clk[1] = __builtin_amdgcn_s_memrealtime() - r0;                                        \
+    }                                                                                        \
+  }
+
 DEFINE_KERNEL(k_fma, OP_FMA)
 DEFINE_KERNEL(k_and, OP_AND)
 DEFINE_KERNEL(k_lshl, OP_LSHL)
 DEFINE_KERNEL(k_bitop3x, OP_BITOP3X)
 DEFINE_KERNEL(k_andor, OP_ANDOR)
 DEFINE_KERNEL(k_or3, OP_OR3)
+DEFINE_MIX(k_mix_ax, OP_MIX_AX)
+DEFINE_MIX(k_mix_a3a, OP_MIX_A3A)
+DEFINE_MIX(k_mix_ab, OP_MIX_AB)
 
 typedef void (*Kern)(uint32_t, uint32_t*, unsigned long long*);
 
@@ -89,7 +113,9 @@ int main() {
             {"v_and_b32", k_and},         {"v_lshlrev_b32", k_lshl},  {"v_add3_u32", k_add3},
             {"v_alignbit_b32", k_align},  {"v_bfi_b32", k_bfi},       {"v_bitop3_b32 (maj)", k_bitop3},
             {"v_bitop3_b32 (xor3)", k_bitop3x}, {"v_and_or_b32", k_andor}, {"v_or3_b32", k_or3},
-            {"v_perm_b32", k_perm}, {"v_lshl_add_u32", k_lshladd}};
+            {"v_perm_b32", k_perm}, {"v_lshl_add_u32", k_lshladd},
+            // mixed streams: is a slow instruction's cost added to a fast one's, or do they overlap?
+            {"mix alignbit+xor", k_mix_ax}, {"mix add3+add", k_mix_a3a}, {"mix alignbit+bitop3", k_mix_ab}};
   double fma_ns[5] = {0, 0, 0, 0, 0};
   for (const K& k : ks) {
     for (int wps : {1, 2, 4}) {  // waves per SIMD: 4 * wps waves per CU
