@@ -947,7 +947,11 @@ def main():
         # at every N, rank 0 alone once the GPU legs are over (the other ranks
         # have left the group), on the same stream as its shard
         sample = min(n_chunks, max(1, GIB // cs))
-        cb = cpu_baseline(args, stream_start, sample, digests[:sample])
+        try:
+            cb = cpu_baseline(args, stream_start, sample, digests[:sample])
+        except Exception as e:  # a host-side failure must not cost the line its device-resident value
+            cb = {"value": None, "unit": "GiB/s", "cores": None, "kind": "port",
+                  "error": f"{type(e).__name__}: {e}", "host": {}}
         if e2e_multi is not None:
             gpu0_numa = e2e_multi["numa_per_rank"][0]["numa_node"]
         if gpu0_numa is not None:

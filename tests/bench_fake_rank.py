@@ -127,6 +127,10 @@ def install():
     bench.DeviceBuffer = FakeDeviceBuffer
     bench.H = fake_H
     bitflood_amd.ChunkHasher = FakeChunkHasher
+    if os.environ.get("FAKE_CPU_BASELINE_FAILS") == "1":
+        def failing_cpu_baseline(*a, **k):
+            raise OSError("injected: the host comparator cannot run")
+        bench.cpu_baseline = failing_cpu_baseline
 
 
 if __name__ == "__main__":

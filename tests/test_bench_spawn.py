@@ -191,3 +191,18 @@ def test_outside_launcher_with_more_ranks_than_gpus_uses_gloo():
     _check_line(out, 2)
     assert out["ranks"]["process_group"] == "gloo"
     assert "process group gloo (rehearsal)" in p.stderr
+
+
+def test_failing_cpu_baseline_still_prints_the_line():
+    """A host-side failure of the CPU comparator (on a node whose host differs
+    from the box's) is recorded in cpu_baseline.error; rank 0 still prints the
+    line with its device-resident value."""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    env.update(RANK="0", LOCAL_RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(bench._free_port()),
+               LBF_BENCH_FORM_GROUP="1", LBF_BENCH_BACKEND="gloo", FAKE_CPU_BASELINE_FAILS="1")
+    p = subprocess.run([sys.executable, FAKE, "--gpus", "1"] + FAKE_ARGV, env=env, capture_output=True, text=True,
+                       timeout=300, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    out = json.loads([x for x in p.stdout.splitlines() if x.strip()][-1])
+    assert out["value"] > 0 and out["roofline"]["achieved"] > 0
+    assert out["cpu_baseline"]["value"] is None and "injected" in out["cpu_baseline"]["error"]
