@@ -43,6 +43,7 @@ import argparse
 import hashlib
 import json
 import os
+import struct
 import sys
 import time
 
@@ -290,32 +291,64 @@ def barrier(world):
         dist.barrier()
 
 
-def traffic_from_profiles(file_bytes, chunk_size, kernel):
+def kernel_code_digest(kernel, lib_path=None):
+    """(mangled symbol, sha256 of its gfx950 machine code) of `kernel` (e.g.
+    'sha1_pc4_kernel<true, 2, 8>') in the library this process loaded
+    (bitflood_amd/kernel_digest.py reads the code object out of the .so), or
+    (None, None) when it cannot be found."""
+    from bitflood_amd import _capi
+    from bitflood_amd import kernel_digest as KD
+    try:
+        d = KD.kernel_digests(lib_path or _capi.LIB_PATH)
+        sym = KD.symbol_for(d, kernel)
+        return (sym, d[sym]) if sym and d.get(sym) else (None, None)
+    except (OSError, ValueError, IndexError, struct.error):
+        return None, None
+
+
+def traffic_from_profiles(file_bytes, chunk_size, kernel, code_sha=None, path=None):
     """HBM bytes per launch measured with rocprofv3 PMC (FETCH_SIZE x2, gfx950
     correction), recorded by tools/pmc_traffic.py --record for
     this workload size and this kernel.  A static lookup, not a measurement of
-    this run: it goes null when the kernel or the size differ."""
-    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    this run, so it is tied to the code it measured: an entry counts only when
+    its recorded machine-code digest (`code_sha256`, the profiled library's
+    bytes for that kernel) equals `code_sha`, the digest of the kernel in the
+    library this run loaded.  Returns (bytes, source, None) or
+    (None, None, reason)."""
+    p = path or os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(p) as f:
             d = json.load(f)
-        for e in d.get("entries", [d]):
-            if (int(e.get("file_bytes", -1)) == int(file_bytes) and int(e.get("chunk_size", 262144)) == chunk_size
-                    and kernel in e.get("kernel", "")):
-                src = e.get("source", p)
-                b = e.get("bench_same_session")
-                if b and e.get("trace_timed_median_ns"):
-                    src += (f" (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE of this kernel at this size; recorded in one lease "
-                            f"with an unprofiled bench line of ms_per_step {b['ms_per_step']} and a kernel trace whose "
-                            f"timed dispatches have median {e['trace_timed_median_ns'] / 1e6:.4f} ms; a lookup, not "
-                            "this run's counters)")
-                else:
-                    src += (" (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, same kernel and size; a recorded lookup, not "
-                            "this run's counters)")
-                return float(e["hbm_bytes_per_launch"]), src
-    except Exception:
-        pass
-    return None, None
+    except (OSError, ValueError) as e:
+        return None, None, f"no traffic record ({type(e).__name__})"
+    reason = f"no PMC record for {kernel} at {file_bytes} B / {chunk_size} B chunks"
+    for e in d.get("entries", [d]):
+        if not (int(e.get("file_bytes", -1)) == int(file_bytes) and int(e.get("chunk_size", 262144)) == chunk_size
+                and kernel in e.get("kernel", "")):
+            continue
+        rec = e.get("code_sha256")
+        if not rec:
+            reason = f"the PMC record for {kernel} ({e.get('source')}) carries no machine-code digest"
+            continue
+        if code_sha is None:
+            reason = f"the loaded library's code for {kernel} could not be read"
+            continue
+        if rec != code_sha:
+            reason = (f"the loaded library's {kernel} is not the code that was profiled ({e.get('source')}: "
+                      f"sha256 {rec[:16]}..., loaded {code_sha[:16]}...)")
+            continue
+        src = e.get("source", p)
+        b = e.get("bench_same_session")
+        if b and e.get("trace_timed_median_ns"):
+            src += (f" (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE of this kernel at this size; recorded in one lease "
+                    f"with an unprofiled bench line of ms_per_step {b['ms_per_step']} and a kernel trace whose "
+                    f"timed dispatches have median {e['trace_timed_median_ns'] / 1e6:.4f} ms; machine code "
+                    f"sha256 {rec[:16]}... equal to the loaded library's; a lookup, not this run's counters)")
+        else:
+            src += (f" (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, same kernel, size and machine code sha256 "
+                    f"{rec[:16]}...; a recorded lookup, not this run's counters)")
+        return float(e["hbm_bytes_per_launch"]), src, None
+    return None, None, reason
 
 
 def _cgroup_cpu_quota():
@@ -824,7 +857,8 @@ def main():
     variant = H.load().lbf_kernel_for(n_chunks)
     floor_ms = compute_floor_ms(variant, cs, n_chunks)
     kernel = KERNELS.get(variant, str(variant))
-    traffic, traffic_src = traffic_from_profiles(file_bytes, cs, kernel)
+    code_sym, code_sha = kernel_code_digest(kernel)
+    traffic, traffic_src, traffic_null = traffic_from_profiles(file_bytes, cs, kernel, code_sha)
     out = None
     if rank == 0:
         c2 = (file_bytes, cs) == (4 * GIB, 262144)
@@ -865,6 +899,9 @@ def main():
                 "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
                 "traffic_source": traffic_src,
+                "traffic_null_reason": traffic_null,
+                "kernel_code_sha256": code_sha,
+                "kernel_symbol": code_sym,
                 "kernel_ms": round(launch_s * 1e3, 4),
                 "algorithmic_bytes_per_launch": file_bytes,
                 # what the HBM fraction can reach at all: SHA-1 is a serial chain per

@@ -34,10 +34,22 @@
 // Prints one JSON line: payload rate, verify latency (frame arrival -> GPU
 // verdict) and accept latency (arrival -> chunk written), batch sizes, and the end
 // state (resume verify of the written file, byte comparison with the source).
+//
+// Process shape (--role).  The reference's peers are separate OS processes, two
+// test_client runs (test_client.cpp:27-77) on one box, each with its own select
+// loop.  --role seeder and --role leecher are those two
+// processes: each owns its HIP runtime, its GPU contexts, its arenas and their
+// registrations, and neither sees the other's.  The seeder writes the flood file
+// (test_encoder's part) into --dir, listens on 127.0.0.1 (--port, 0 = any) and
+// writes the port to --port-file once it is listening; the leecher loads the
+// flood file from --dir and connects to --port.  Each prints its own JSON line
+// (tests/test_host_cpp.py merges them).  The default, --role both, runs the two
+// peers as threads of one process, the round-1 to round-4 harness.
 #include <arpa/inet.h>
 #include <fcntl.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
+#include <poll.h>
 #include <sys/socket.h>
 #include <sys/stat.h>
 #include <sys/statvfs.h>
@@ -86,6 +98,9 @@ struct Opts {
   bool gpu_decode = true;        // the leecher's base64 decode on the GPU with its verify (--cpu-decode: on the host)
   bool gpu_encode = false;       // --gpu-encode: the seeder's base64 encode on the GPU with its verify (--synthetic)
   unsigned seeder_workers = 1;   // --seeder-workers S: the seeder's verify/encode workers (each its own context)
+  enum Role { BOTH, SEEDER, LEECHER } role = BOTH;  // --role: both peers in this process, or one of them
+  int port = -1;                 // seeder: port to listen on (0 / unset = any); leecher: port to dial
+  std::string port_file;         // seeder: where to write the port once listening
 };
 
 [[noreturn]] void die(const std::string& m) {
@@ -195,7 +210,7 @@ int listen_loopback(int& port) {
   sockaddr_in a{};
   a.sin_family = AF_INET;
   a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
-  a.sin_port = 0;
+  a.sin_port = htons((uint16_t)(port > 0 ? port : 0));
   if (bind(fd, (sockaddr*)&a, sizeof(a)) != 0 || listen(fd, 1) != 0) die("bind/listen on 127.0.0.1 failed");
   socklen_t len = sizeof(a);
   getsockname(fd, (sockaddr*)&a, &len);
@@ -426,6 +441,9 @@ struct Chan {
 // encoder then compete for the same cores, so it is not the
 // default.
 void seeder_main(int lfd, FloodFileSPtr ff, std::string root, const Opts& o, SeederStats& st) {
+  // a seeder process whose leecher never comes must still end
+  pollfd pl{lfd, POLLIN, 0};
+  if (poll(&pl, 1, 300 * 1000) != 1) die("seeder: no leecher connected within 300 s");
   const int fd = accept(lfd, nullptr, nullptr);
   if (fd < 0) die("accept failed");
   tune(fd);
@@ -693,13 +711,23 @@ int main(int argc, char** argv) {
     else if (a == "--seeder-workers") o.seeder_workers = (unsigned)strtoul(val(), nullptr, 10);
     else if (a == "--gpu-encode") o.gpu_encode = true;
     else if (a == "--cpu-encode") o.gpu_encode = false;
+    else if (a == "--role") {
+      const std::string r = val();
+      if (r == "both") o.role = Opts::BOTH;
+      else if (r == "seeder") o.role = Opts::SEEDER;
+      else if (r == "leecher") o.role = Opts::LEECHER;
+      else die("--role takes both, seeder or leecher");
+    } else if (a == "--port") o.port = (int)strtol(val(), nullptr, 10);
+    else if (a == "--port-file") o.port_file = val();
     else {
       fprintf(stderr,
               "usage: lbf_loopback [--size BYTES] [--chunksize N] [--window W] [--batch B] [--deadline-ms MS]\n"
               "                    [--threads T]\n"
               "                    [--corrupt K] [--dir DIR] [--keep] [--synthetic] [--no-register]\n"
               "                    [--verifiers V] [--pipelined-seeder] [--gpu-decode | --cpu-decode]\n"
-              "                    [--gpu-encode | --cpu-encode] [--seeder-workers S]\n");
+              "                    [--gpu-encode | --cpu-encode] [--seeder-workers S]\n"
+              "                    [--role both | --role seeder [--port P] [--port-file F] |\n"
+              "                     --role leecher --port P]   (seeder and leecher: same --dir and options)\n");
       return 2;
     }
   }
@@ -707,6 +735,9 @@ int main(int argc, char** argv) {
   if (o.verifiers == 0 || o.verifiers > 8) die("verifiers must be 1..8");
   if (o.seeder_workers == 0 || o.seeder_workers > 8) die("seeder workers must be 1..8");
   if (o.gpu_encode && !o.synthetic) die("--gpu-encode needs --synthetic (the file seeder reads and verifies in one call)");
+  if (o.role != Opts::BOTH && o.dir.empty()) die("--role seeder/leecher needs --dir (the directory both peers share)");
+  if (o.role == Opts::LEECHER && (o.port <= 0 || o.port > 65535)) die("--role leecher needs --port");
+  if (o.port > 65535) die("--port must be 0..65535");
   if (o.dir.empty()) {
     const char* t = getenv("TMPDIR");
     char tmpl[512];
@@ -714,47 +745,91 @@ int main(int argc, char** argv) {
     if (!mkdtemp(tmpl)) die("mkdtemp failed");
     o.dir = tmpl;
   }
+  const bool is_seeder = o.role != Opts::LEECHER, is_leecher = o.role != Opts::SEEDER;
   const std::string seeddir = o.dir + "/seed", leechdir = o.dir + "/leech";
   mkdir(o.dir.c_str(), 0755);
-  mkdir(seeddir.c_str(), 0755);
-  mkdir(leechdir.c_str(), 0755);
+  if (is_seeder) mkdir(seeddir.c_str(), 0755);
+  if (is_leecher) mkdir(leechdir.c_str(), 0755);
   struct statvfs vfs;
-  const U64 copies = o.synthetic ? 1 : 2;
+  // the bytes this process writes: the seeder's file (not with --synthetic), the leecher's copy
+  const U64 copies = (is_seeder && !o.synthetic ? 1 : 0) + (is_leecher ? 1 : 0);
   if (statvfs(o.dir.c_str(), &vfs) == 0 && (U64)vfs.f_bavail * vfs.f_frsize < copies * o.size + (64 << 20))
     die("not enough free space in " + o.dir + " for " + std::to_string(copies) + " copies of the file");
 
   // The seeder's file and the flood file both peers load (test_encoder + test_client).
   const std::string name = "c5.bin";
-  FloodFile encoded;
-  auto te0 = Clock::now();
-  if (o.synthetic) {
-    encode_synthetic(seeddir + "/" + name, o.size, o.chunksize, encoded);
-  } else {
-    write_source(seeddir + "/" + name, o.size, o.threads);
-    te0 = Clock::now();
-    Encoder::ToEncode te;
-    te.m_files.push_back(seeddir + "/" + name);
-    te.m_chunksize = o.chunksize;
-    if (Encoder::EncodeFile(te, encoded) != Error::NO_ERROR_LBF)
-      die("EncodeFile failed: " + std::string(Encoder::LastError()));
-  }
-  const double encode_s = secs(te0, Clock::now());
-  // peers address the file by its name relative to their own directory
-  FloodFileSPtr ff(new FloodFile());
-  for (auto& kv : encoded.m_files) {
-    FloodFile::FileSPtr file = kv.second;
-    file->m_name = name;
-    ff->m_files[name] = file;
-  }
   const std::string floodpath = o.dir + "/c5.flood";
-  if (ff->ToXMLFile(floodpath) != Error::NO_ERROR_LBF) die("ToXMLFile failed");
+  double encode_s = 0;
+  FloodFileSPtr ff(new FloodFile());
+  if (is_seeder) {
+    FloodFile encoded;
+    auto te0 = Clock::now();
+    if (o.synthetic) {
+      encode_synthetic(seeddir + "/" + name, o.size, o.chunksize, encoded);
+    } else {
+      write_source(seeddir + "/" + name, o.size, o.threads);
+      te0 = Clock::now();
+      Encoder::ToEncode te;
+      te.m_files.push_back(seeddir + "/" + name);
+      te.m_chunksize = o.chunksize;
+      if (Encoder::EncodeFile(te, encoded) != Error::NO_ERROR_LBF)
+        die("EncodeFile failed: " + std::string(Encoder::LastError()));
+    }
+    encode_s = secs(te0, Clock::now());
+    // peers address the file by its name relative to their own directory
+    for (auto& kv : encoded.m_files) {
+      FloodFile::FileSPtr file = kv.second;
+      file->m_name = name;
+      ff->m_files[name] = file;
+    }
+    if (ff->ToXMLFile(floodpath) != Error::NO_ERROR_LBF) die("ToXMLFile failed");
+  }
+
+  int port = o.port > 0 ? o.port : 0;
+  const int lfd = is_seeder ? listen_loopback(port) : -1;
+  SeederStats sst;
+  if (o.role == Opts::SEEDER) {
+    // The flood file is complete before the port is published, so a leecher
+    // started on the port file finds it.  Written then renamed: never half a number.
+    if (!o.port_file.empty()) {
+      const std::string tmp = o.port_file + ".tmp";
+      FILE* pf = fopen(tmp.c_str(), "w");
+      if (!pf || fprintf(pf, "%d\n", port) < 0 || fclose(pf) != 0 || rename(tmp.c_str(), o.port_file.c_str()) != 0)
+        die("cannot write the port file " + o.port_file);
+    }
+    fprintf(stderr, "lbf_loopback: seeder listening on 127.0.0.1:%d\n", port);
+    const auto s0 = Clock::now();
+    seeder_main(lfd, ff, seeddir, o, sst);
+    const double serve_s = secs(s0, Clock::now());
+    close(lfd);
+    printf("{\"config\": \"C5 loopback 2-peer\", \"role\": \"seeder\", \"pid\": %d, \"bytes\": %llu, "
+           "\"chunk_size\": %u, \"chunks\": %zu, \"batch\": %u, \"seeder_pipelined\": %s, \"gpu_encode\": %s, "
+           "\"seeder_workers\": %u, \"threads\": %u, \"seconds\": %.3f, \"encode_flood_s\": %.3f, "
+           "\"seeder\": {\"requests\": %llu, \"sent\": %llu, \"refused\": %llu, \"verify_s\": %.3f, "
+           "\"encode_s\": %.3f}, \"corrupt_every\": %u, \"corrupted_sent\": %llu, \"seed_source\": \"%s\", "
+           "\"arenas_registered\": %s}\n",
+           (int)getpid(), (unsigned long long)o.size, o.chunksize,
+           ff->m_files.empty() ? (size_t)0 : ff->m_files.begin()->second->m_chunks.size(), o.batch,
+           o.seeder_pipeline ? "true" : "false", o.gpu_encode ? "true" : "false", o.seeder_workers, o.threads,
+           serve_s, encode_s, (unsigned long long)sst.requests, (unsigned long long)sst.sent,
+           (unsigned long long)sst.refused, sst.verify_s, sst.encode_s, o.corrupt, (unsigned long long)sst.corrupted,
+           o.synthetic ? "synthetic stream (generated on request, no seeder file)" : "file",
+           o.register_arenas ? "true" : "false");
+    fflush(stdout);
+    // the leecher has compared its copy before it closed the connection
+    if (!o.keep) {
+      unlink((seeddir + "/" + name).c_str());
+      unlink(floodpath.c_str());
+      if (!o.port_file.empty()) unlink(o.port_file.c_str());
+      rmdir(seeddir.c_str());
+      rmdir(o.dir.c_str());  // whichever peer ends last removes it
+    }
+    return 0;
+  }
+  std::thread seeder;
+  if (o.role == Opts::BOTH) seeder = std::thread(seeder_main, lfd, ff, seeddir, std::cref(o), std::ref(sst));
   FloodFileSPtr leech_ff(new FloodFile());
   if (leech_ff->FromXMLFile(floodpath) != Error::NO_ERROR_LBF) die("FromXMLFile failed");
-
-  int port = 0;
-  const int lfd = listen_loopback(port);
-  SeederStats sst;
-  std::thread seeder(seeder_main, lfd, ff, seeddir, std::cref(o), std::ref(sst));
 
   Flood fl;
   fl.m_rootdir = leechdir;
@@ -1046,18 +1121,32 @@ int main(int argc, char** argv) {
   for (unsigned v = 1; v < o.verifiers; ++v) lbf_ctx_destroy(vctx[v]);
   free(arena_mem);
   free(text_mem);
-  shutdown(fd, SHUT_RDWR);
-  reader.join();
-  close(fd);
-  seeder.join();
-  close(lfd);
 
-  // end state: what a restarted leecher would find (Flood::_SetupFilesAndChunks)
+  // end state: what a restarted leecher would find (Flood::_SetupFilesAndChunks),
+  // checked while the connection is still open, so a seeder process (which
+  // removes its file once the leecher hangs up) still has its copy for the comparison
   Flood check;
   check.m_rootdir = leechdir;
   const bool resumed = check.Initialize(leech_ff) == Error::NO_ERROR_LBF && check.m_chunkstodownload.empty();
   const bool same = o.synthetic ? file_matches_synthetic(leechdir + "/" + name, o.size, o.threads)
                                 : files_equal(seeddir + "/" + name, leechdir + "/" + name);
+  shutdown(fd, SHUT_RDWR);
+  reader.join();
+  close(fd);
+  if (seeder.joinable()) seeder.join();
+  if (lfd >= 0) close(lfd);
+  // a leecher process reports the seeder's side as null: the seeder process prints it
+  char seeder_json[512];
+  if (o.role == Opts::BOTH)
+    snprintf(seeder_json, sizeof(seeder_json),
+             "{\"requests\": %llu, \"sent\": %llu, \"refused\": %llu, \"verify_s\": %.3f, \"encode_s\": %.3f}",
+             (unsigned long long)sst.requests, (unsigned long long)sst.sent, (unsigned long long)sst.refused,
+             sst.verify_s, sst.encode_s);
+  else
+    snprintf(seeder_json, sizeof(seeder_json), "null");
+  char corrupted_json[32];
+  if (o.role == Opts::BOTH) snprintf(corrupted_json, sizeof(corrupted_json), "%llu", (unsigned long long)sst.corrupted);
+  else snprintf(corrupted_json, sizeof(corrupted_json), "null");
   std::sort(lat_us.begin(), lat_us.end());
   std::sort(acc_us.begin(), acc_us.end());
   auto pct_of = [](const std::vector<double>& v, double p) {
@@ -1065,35 +1154,38 @@ int main(int argc, char** argv) {
   };
   auto pct = [&](double p) { return pct_of(lat_us, p); };
   const double wall = secs(t_start, t_end);
-  printf("{\"config\": \"C5 loopback 2-peer\", \"bytes\": %llu, \"chunk_size\": %u, \"chunks\": %zu, "
+  printf("{\"config\": \"C5 loopback 2-peer\", \"role\": \"%s\", \"pid\": %d, \"bytes\": %llu, \"chunk_size\": %u, "
+         "\"chunks\": %zu, "
          "\"window\": %u, \"batch\": %u, \"deadline_ms\": %u, \"verifiers\": %u, \"seeder_pipelined\": %s, "
          "\"gpu_decode\": %s, \"gpu_encode\": %s, \"seeder_workers\": %u, "
          "\"threads\": %u, \"seconds\": %.3f, \"payload_gibs\": %.3f, "
          "\"wire_gibs\": %.3f, \"encode_flood_s\": %.3f, "
          "\"leecher\": {\"batches\": %zu, \"mean_batch\": %.1f, \"decode_s\": %.3f, \"verify_s\": %.3f, "
          "\"write_s\": %.3f, "
-         "\"rejected\": %zu, \"undecodable\": %zu}, \"seeder\": {\"requests\": %llu, \"sent\": %llu, \"refused\": %llu, \"verify_s\": %.3f, "
-         "\"encode_s\": %.3f}, \"verify_latency_us\": {\"p50\": %.0f, \"p90\": %.0f, \"p99\": %.0f, \"max\": %.0f}, "
+         "\"rejected\": %zu, \"undecodable\": %zu}, \"seeder\": %s, "
+         "\"verify_latency_us\": {\"p50\": %.0f, \"p90\": %.0f, \"p99\": %.0f, \"max\": %.0f}, "
          "\"accept_latency_us\": {\"p50\": %.0f, \"p90\": %.0f, \"p99\": %.0f, \"max\": %.0f}, "
-         "\"resume_verify_complete\": %s, \"files_identical\": %s, \"corrupt_every\": %u, \"corrupted_sent\": %llu, "
+         "\"resume_verify_complete\": %s, \"files_identical\": %s, \"corrupt_every\": %u, \"corrupted_sent\": %s, "
          "\"seed_source\": \"%s\", \"arenas_registered\": %s}\n",
-         (unsigned long long)o.size, o.chunksize, total, o.window, o.batch, o.deadline_ms, o.verifiers,
+         o.role == Opts::BOTH ? "both" : "leecher", (int)getpid(), (unsigned long long)o.size, o.chunksize, total,
+         o.window, o.batch, o.deadline_ms, o.verifiers,
          o.seeder_pipeline ? "true" : "false", o.gpu_decode ? "true" : "false",
          o.gpu_encode ? "true" : "false", o.seeder_workers, o.threads, wall,
          payload / wall / (1u << 30), wire_bytes / wall / (1u << 30), encode_s, batches,
          batches ? (double)(accepted + rejected) / batches : 0.0, decode_s, verify_s, write_s, rejected, undecodable,
-         (unsigned long long)sst.requests, (unsigned long long)sst.sent, (unsigned long long)sst.refused, sst.verify_s,
-         sst.encode_s, pct(0.5), pct(0.9), pct(0.99), lat_us.empty() ? 0.0 : lat_us.back(), pct_of(acc_us, 0.5),
+         seeder_json, pct(0.5), pct(0.9), pct(0.99), lat_us.empty() ? 0.0 : lat_us.back(), pct_of(acc_us, 0.5),
          pct_of(acc_us, 0.9), pct_of(acc_us, 0.99), acc_us.empty() ? 0.0 : acc_us.back(), resumed ? "true" : "false",
-         same ? "true" : "false", o.corrupt, (unsigned long long)sst.corrupted,
+         same ? "true" : "false", o.corrupt, corrupted_json,
          o.synthetic ? "synthetic stream (generated on request, no seeder file)" : "file",
          o.register_arenas ? "true" : "false");
   if (!o.keep) {
-    unlink((seeddir + "/" + name).c_str());
     unlink((leechdir + "/" + name).c_str());
-    unlink(floodpath.c_str());
-    rmdir(seeddir.c_str());
     rmdir(leechdir.c_str());
+    if (o.role == Opts::BOTH) {  // a seeder process removes its own files
+      unlink((seeddir + "/" + name).c_str());
+      unlink(floodpath.c_str());
+      rmdir(seeddir.c_str());
+    }
     rmdir(o.dir.c_str());
   }
   return resumed && same ? 0 : 1;

@@ -18,6 +18,7 @@ import numpy as np
 import pytest
 
 from bitflood_amd import _capi
+from tests.c5_pair import run_pair
 from tests.domwriter import pretty
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -84,18 +85,29 @@ def test_loopback_needs_gpu():
 
 
 def _loopback(tmp_path, size, cs, window, batch, corrupt, synthetic=False, threads=None, timeout=600, register=True,
-              extra=()):
-    args = [os.path.join(LIB, "lbf_loopback"), "--size", str(size), "--chunksize", str(cs), "--window", str(window),
-            "--batch", str(batch), "--corrupt", str(corrupt), "--dir", str(tmp_path / "c5")] + list(extra)
+              extra=(), shape="one process"):
+    """shape "one process": both peers as threads of one lbf_loopback (--role
+    both); "two processes": the reference's shape, a seeder process and a
+    leecher process (tests/c5_pair.py), each with its own HIP runtime."""
+    opts = ["--size", str(size), "--chunksize", str(cs), "--window", str(window),
+            "--batch", str(batch), "--corrupt", str(corrupt)] + list(extra)
     if synthetic:
-        args.append("--synthetic")
+        opts.append("--synthetic")
     if threads:
-        args += ["--threads", str(threads)]
+        opts += ["--threads", str(threads)]
     if not register:
-        args.append("--no-register")
-    out = subprocess.run(args, capture_output=True, text=True, timeout=timeout)
-    assert out.returncode == 0, out.stderr + out.stdout
-    r = json.loads(out.stdout.strip().splitlines()[-1])
+        opts.append("--no-register")
+    if shape == "two processes":
+        r, _, _ = run_pair(opts, str(tmp_path / "c5"), timeout=timeout)
+        assert r["pids"]["seeder"] != r["pids"]["leecher"]
+        assert not os.path.exists(tmp_path / "c5"), "the two peers left files behind"
+    else:
+        out = subprocess.run([os.path.join(LIB, "lbf_loopback")] + opts + ["--dir", str(tmp_path / "c5")],
+                             capture_output=True, text=True, timeout=timeout)
+        assert out.returncode == 0, out.stderr + out.stdout
+        r = json.loads(out.stdout.strip().splitlines()[-1])
+        assert r["role"] == "both"
+        r["process_shape"] = "one process"
     assert r["resume_verify_complete"] and r["files_identical"]
     assert r["arenas_registered"] is register
     n = (size + cs - 1) // cs
@@ -126,6 +138,39 @@ def test_loopback_two_peers(tmp_path, size, cs, window, batch, corrupt, syntheti
     equals the source (a file, or with --synthetic the generated stream) byte
     for byte."""
     _loopback(tmp_path, size, cs, window, batch, corrupt, synthetic)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("size,cs,window,batch,corrupt,synthetic,extra", [
+    (64 << 20, 262144, 64, 16, 0, False, []),
+    ((16 << 20) + 12345, 65536, 512, 128, 7, False, []),                 # file seeder, odd tail, wire errors
+    ((16 << 20) + 12345, 65536 + 3, 512, 128, 7, True, []),              # generated seeder, off the 8-byte grid
+    (65537, 4096, 1, 3, 1, True, []),                                    # every chunk corrupted once
+    (0, 1000, 1024, 512, 0, True, []),                                   # empty file
+    ((32 << 20) + 12345, 65536, 512, 128, 7, True, ["--gpu-encode", "--seeder-workers", "2"]),
+    ((32 << 20) + 12345, 65536, 512, 128, 7, False, ["--verifiers", "1", "--cpu-decode", "--no-register"]),
+])
+def test_loopback_two_processes(tmp_path, size, cs, window, batch, corrupt, synthetic, extra):
+    """The reference's process shape: seeder and leecher are
+    separate processes sharing the GPU, each with its own HIP runtime, GPU
+    contexts and pinned arenas (neither sees the other's registrations).  Same
+    end state as the one-process harness: the written file equals the source,
+    every corrupted arrival is rejected and fetched again."""
+    register = "--no-register" not in extra
+    r = _loopback(tmp_path, size, cs, window, batch, corrupt, synthetic, register=register,
+                  extra=[e for e in extra if e != "--no-register"], shape="two processes")
+    assert r["seeder"]["sent"] >= r["chunks"]
+
+
+def test_loopback_role_options_checked_before_the_gpu(tmp_path):
+    """--role errors are reported before any GPU call (CPU-only host)."""
+    lb = os.path.join(LIB, "lbf_loopback")
+    for args, msg in [(["--role", "leecher", "--dir", str(tmp_path)], "needs --port"),
+                      (["--role", "seeder"], "needs --dir"),
+                      (["--role", "peer"], "--role takes"),
+                      (["--role", "seeder", "--dir", str(tmp_path), "--port", "70000"], "--port must be")]:
+        out = subprocess.run([lb] + args, capture_output=True, text=True, timeout=60)
+        assert out.returncode == 2 and msg in out.stderr, (args, out.stderr)
 
 
 @pytest.mark.gpu
@@ -165,19 +210,24 @@ def test_loopback_staged_arenas(tmp_path):
 
 @pytest.mark.gpu
 @pytest.mark.timeout(900)
-def test_c5_full_size_16gib(tmp_path):
+@pytest.mark.parametrize("shape", ["two processes", "one process"])
+def test_c5_full_size_16gib(tmp_path, shape):
     """C5 at its stated workload (BASELINE.json configs[4]): 16 GiB at the
     test_encoder default of 256 KiB chunks, i.e. 65,536 chunks, each verified on
     the GPU on receipt (ChunkMethods.cpp:137-225) before it is written, with
     every 1000th chunk corrupted on the wire once.  The seeder serves the
     generated stream (no 16 GiB seeder file); the leecher's 16 GiB file must pass
-    the resume verify and equal the stream.  Not in the harness, on purpose: the
+    the resume verify and equal the stream.  "two processes" is the config's own
+    shape (two test_client processes): each peer a fresh process
+    with its own HIP runtime on the one GPU; "one process" is the threaded
+    harness.  Not in the harness, on purpose: the
     tracker hop (test_tracker.cpp:27-75, TrackerMethods.cpp:26-44), the
     NotifyHaveChunk broadcast (ChunkMethods.cpp:202-211) and the 100 ms loop
     pacing (test_client.cpp:72-76) -- control plane, not the hash path."""
-    r = _loopback(tmp_path, 16 << 30, 262144, 4096, 1024, 1000, synthetic=True, threads=16, timeout=840)
-    print("C5 16 GiB:", json.dumps({k: r[k] for k in ("seconds", "payload_gibs", "wire_gibs", "verify_latency_us",
-                                                        "accept_latency_us", "leecher", "seeder", "encode_flood_s")}))
+    r = _loopback(tmp_path, 16 << 30, 262144, 4096, 1024, 1000, synthetic=True, threads=16, timeout=840, shape=shape)
+    print(f"C5 16 GiB ({shape}):", json.dumps({k: r[k] for k in (
+        "seconds", "payload_gibs", "wire_gibs", "verify_latency_us", "accept_latency_us", "leecher", "seeder",
+        "encode_flood_s", "process_shape")}))
     assert r["chunks"] == 65536 and r["corrupted_sent"] == 65
     # Latency at the default 10 ms batch deadline (DESIGN.md §5.1): verify =
     # frame arrival -> GPU verdict (before the disk write), accept = arrival ->

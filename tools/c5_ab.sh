@@ -11,7 +11,9 @@
 # seeder workers; sw2e = sw2 with --gpu-encode; sw3 = gd with three seeder workers;
 # gd3 / gd4 = gd with three / four leecher verifiers;
 # pre = v2s run by bitflood_amd/lib/lbf_loopback_prepool when that binary exists
-# (a build of an earlier lbf_loopback.cpp, for an A/B across a harness change).
+# (a build of an earlier lbf_loopback.cpp, for an A/B across a harness change);
+# 1p / 2p = the defaults as one process (--role both) / as the reference's two
+# processes, a seeder process and a leecher process (tests/c5_pair.py).
 set -o pipefail
 tag=${1:-c5ab}
 rounds=${2:-2}
@@ -25,13 +27,15 @@ declare -A flags=([r03]="--verifiers 1 --cpu-decode" [v1]="--verifiers 1 --pipel
                   [ge]="--verifiers 2 --gpu-decode --gpu-encode" \
                   [sw2]="--verifiers 2 --seeder-workers 2" [sw2e]="--verifiers 2 --seeder-workers 2 --gpu-encode" \
                   [sw3]="--verifiers 2 --seeder-workers 3" \
-                  [gd3]="--verifiers 3" [gd4]="--verifiers 4" [pre]="--verifiers 2")
+                  [gd3]="--verifiers 3" [gd4]="--verifiers 4" [pre]="--verifiers 2" [1p]="" [2p]="")
 for r in $(seq "$rounds"); do
   for v in $variants; do
     bin=bitflood_amd/lib/lbf_loopback
     if [ "$v" = pre ]; then bin=bitflood_amd/lib/lbf_loopback_prepool; fi
-    line=$(timeout -k 10 240 $bin --size $((16 << 30)) --chunksize 262144 --window 4096 \
-      --batch 1024 --corrupt 1000 --synthetic --threads 16 --dir "$TMPDIR/c5ab" ${flags[$v]} 2> "$out/$v.$r.err") \
+    run=$bin
+    if [ "$v" = 2p ]; then run="python3 -m tests.c5_pair"; fi
+    line=$(timeout -k 10 240 $run --size $((16 << 30)) --chunksize 262144 --window 4096 \
+      --batch 1024 --corrupt 1000 --synthetic --threads 16 $([ "$v" = 2p ] || echo --dir "$TMPDIR/c5ab") ${flags[$v]} 2> "$out/$v.$r.err") \
       || { echo "run $v.$r failed rc=$?"; tail -5 "$out/$v.$r.err"; exit 1; }
     echo "{\"variant\": \"$v\", \"round\": $r, \"run\": $line}" >> "$out/c5_ab.jsonl"
     echo "$v.$r done"

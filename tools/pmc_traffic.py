@@ -11,7 +11,10 @@ the wave-cycle split (active / waiting on memory / issue-stalled).
 
 Usage: tools/pmc_traffic.py gpurun_out/prof/<tag> profiles/<round>/<tag> [--file-bytes N]
 Writes <dst>/summary.json, copies the kernel-stats CSV, and (with
---record) updates profiles/pmc_traffic.json read by bench.py.
+--record) updates profiles/pmc_traffic.json read by bench.py.  Each record
+carries the machine-code digest of the profiled kernel (code_sha256, from the
+same lease's bench line); bench.py cites the traffic only while the library it
+loads carries that same code.
 """
 import argparse
 import collections
@@ -63,6 +66,10 @@ def main():
         out["bench_same_session"] = {"value": line["value"], "ms_per_step": line["ms_per_step"],
                                      "kernel_ms": line["roofline"]["kernel_ms"], "frac": line["roofline"]["frac"],
                                      "kernel": line["config"]["kernel"]}
+        # the machine code of the kernel the lease ran (bench.py reads it out of the loaded library)
+        if line["roofline"].get("kernel_code_sha256"):
+            out["code_sha256"] = line["roofline"]["kernel_code_sha256"]
+            out["code_symbol"] = line["roofline"].get("kernel_symbol")
     except (OSError, ValueError, KeyError, IndexError):
         pass
     # the bench line the traced run printed (its HIP events include the tracer's overhead)
@@ -155,7 +162,8 @@ def main():
                "hbm_bytes_per_launch": out["hbm_bytes_per_launch"],
                "source": os.path.relpath(os.path.join(a.dst, "summary.json"), root),
                "kernel": out.get("kernel")}
-        for k in ("trace_median_ns", "trace_timed_median_ns", "bench_same_session", "bench_traced_run"):
+        for k in ("code_sha256", "code_symbol", "trace_median_ns", "trace_timed_median_ns", "bench_same_session",
+                  "bench_traced_run"):
             if k in out:
                 rec[k] = out[k]
         try:
