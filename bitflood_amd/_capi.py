@@ -55,6 +55,7 @@ _SIGS = {
     "lbf_host_register": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_uint64]),
     "lbf_host_unregister": (_c.c_int, [_c.c_void_p, _c.c_void_p]),
     "lbf_ctx_staging_stats": (_c.c_int, [_c.c_void_p, _c.POINTER(_c.c_uint64), _c.POINTER(_c.c_uint64)]),
+    "lbf_ctx_b64_stats": (_c.c_int, [_c.c_void_p, _c.POINTER(_c.c_uint64), _c.POINTER(_c.c_uint64)]),
     "lbf_sha1_one": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_uint32, _c.c_void_p]),
     "lbf_verify_encode_b64_batch": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_uint64, _c.c_void_p, _c.c_void_p,
                                                _c.c_uint64, _c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_uint64,

@@ -86,29 +86,99 @@ __device__ __forceinline__ uint32_t wg_exclusive_scan(uint32_t v, uint32_t* sums
 }
 
 // ---------------------------------------------------------------------------
-// One pass for text laid out as the encoder writes it (round 4).  Almost every
-// frame carries exactly what xmlrpc++'s encoder wrote: group g of the chunk at
-// 4g + g/18, a separator (any character outside the alphabet) after every 18th
-// group, '=' only as "xx==" / "xxx=" in the last group.  For such a text the
-// place of every character is known without a scan, so each lane decodes four
-// groups straight from the text into the output: 7/3 bytes moved per decoded
-// byte instead of 5, one pass instead of two, and no workgroup barrier.  The
-// lanes check the layout as they read it; a chunk whose text breaks it
-// anywhere (junk, a dropped or extra character, '=' elsewhere) is marked in
-// redo[] and decoded again by b64_decode_kernel, whose general rules give the
-// same result as this pass on every canonical text.
+// Tiles of whole lines.  The encoder's text is lines of 18 groups: 72 alphabet
+// characters and a separator (base64.h:197-205's '\n', framed as a space), 73
+// characters that decode to 54 bytes.  A tile of 64 lines is 4,672 characters
+// and 3,456 bytes, both multiples of 16, so tile k of a chunk reads text
+// [4672k, +4672) and writes bytes [3456k, +3456) (or the reverse for the
+// encode) with 16-byte accesses whenever the chunk's slot is 16-byte aligned,
+// and no group or separator crosses a tile.  grid.x = chunks x tiles; every
+// workgroup stages its tile's input span in LDS with coalesced 16-byte loads
+// (global_load_dwordx4 + ds_write_b128), then each lane builds one 16-byte
+// block of the output from LDS and stores it: one pass over HBM in each
+// direction, nothing re-read.  (Round 4's kernels read bytes straight from HBM,
+// 16 byte loads per four groups per lane, and spent 74-86 % of their wave
+// cycles waiting on memory at 0.23-0.30 of the HBM peak)
+// ---------------------------------------------------------------------------
+constexpr uint32_t kB64TileLines = 64;
+constexpr uint32_t kB64TileText = kB64TileLines * 73;    // 4,672 characters
+constexpr uint32_t kB64TileBytes = kB64TileLines * 54;   // 3,456 bytes
+constexpr uint32_t kB64TileGroups = kB64TileLines * 18;  // 1,152 groups
+static_assert(kB64TileText % 16 == 0 && kB64TileBytes % 16 == 0, "tiles of 16-byte blocks");
+typedef uint32_t b64_u32x4 __attribute__((ext_vector_type(4)));  // what the nontemporal builtins take
+
+// Stage global bytes [src, src + len) in LDS as the aligned 16-byte blocks that
+// hold them: afterwards lds byte (delta + k) = src[k], delta = src mod 16.  The
+// blocks are read whole (a 16-byte block holding one byte of the span lies in
+// the same page, so this never reads an unmapped address).  Up to two blocks
+// per lane, both loads issued before either store.
+template <uint32_t kBlocks>
+__device__ __forceinline__ uint32_t b64_stage_span(const uint8_t* src, uint32_t len, uint4* lds) {
+  static_assert(kBlocks <= 2 * kB64Threads, "two blocks per lane at most");
+  const uintptr_t a = reinterpret_cast<uintptr_t>(src);
+  const uint32_t delta = (uint32_t)(a & 15u);
+  const b64_u32x4* g = reinterpret_cast<const b64_u32x4*>(a - delta);
+  b64_u32x4* l = reinterpret_cast<b64_u32x4*>(lds);
+  const uint32_t blocks = (delta + len + 15) / 16;
+  const uint32_t k0 = threadIdx.x, k1 = threadIdx.x + kB64Threads;
+  b64_u32x4 v0, v1;
+  if (k0 < blocks) v0 = __builtin_nontemporal_load(g + k0);
+  if (k1 < blocks) v1 = __builtin_nontemporal_load(g + k1);
+  if (k0 < blocks) l[k0] = v0;
+  if (k1 < blocks) l[k1] = v1;
+  return delta;
+}
+
+// Four bytes of LDS from any byte address (two aligned dword reads + v_alignbyte).
+__device__ __forceinline__ uint32_t lds_u32_at(const uint32_t* w, uint32_t at) {
+  return __builtin_amdgcn_alignbyte(w[(at >> 2) + 1], w[at >> 2], at & 3u);
+}
+
+// Store a 16-byte block to dst = base + pos, clipped to [0, end) of the slot:
+// one 16-byte store when it is whole and aligned, bytes otherwise.
+__device__ __forceinline__ void b64_put_block(uint8_t* base, uint64_t pos, uint64_t end, uint4 v) {
+  uint8_t* dst = base + pos;
+  if (pos + 16 <= end && (reinterpret_cast<uintptr_t>(dst) & 15u) == 0) {
+    const b64_u32x4 x = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(x, reinterpret_cast<b64_u32x4*>(dst));
+    return;
+  }
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  for (uint32_t m = 0; m < 16 && pos + m < end; ++m) dst[m] = (uint8_t)(w[m >> 2] >> (8 * (m & 3)));
+}
+
+// ---------------------------------------------------------------------------
+// One pass for text laid out as the encoder writes it (round 4; tiled in
+// round 5).  Almost every frame carries exactly what xmlrpc++'s encoder
+// wrote: group g of the chunk at 4g + g/18, a separator (any character outside
+// the alphabet) after every 18th group, '=' only as "xx==" / "xxx=" in the
+// last group.  For such a text the place of every character is known without
+// a scan.  The lanes check the layout as they read it; a chunk whose text
+// breaks it anywhere (junk, a dropped or extra character, '=' elsewhere) is
+// marked in redo[] and decoded again by b64_decode_kernel, whose general rules
+// give the same result as this pass on every canonical text.
 //
-// A canonical text of G groups has length L = 73 q + 4 r for G = 18 q + r,
-// r < 18, so G follows from L alone.  grid = (chunks, parts): part y of chunk
-// i takes tasks [y * per, (y + 1) * per) of four groups each.
+// The length gives the group count.  The encoder writes a separator after
+// every 18th complete group, so a text of G = 18q + r groups (0 < r < 18 or
+// r = 0) has length 73q + 4r, and one whose last, padded group is the 18th of
+// its line has no separator after it: 73q + 72, G = 18(q + 1).
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ bool b64_canon_groups(uint32_t len, uint32_t* groups) {
   const uint32_t q = len / 73, rem = len % 73;
-  if (rem % 4 != 0 || rem / 4 >= 18) return false;
+  if (rem == 72) {  // the last line's 18th group is the padded last group
+    *groups = 18 * q + 18;
+    return true;
+  }
+  if (rem % 4 != 0) return false;
   *groups = 18 * q + rem / 4;
   return true;
 }
 
+// blockIdx.x = (chunk - chunk0) * tiles + tile.  Chunk i's text is
+// text[text_off[i] .. + text_len[i]); its decoded bytes go to
+// out[out_off[i] .. + cap[i]): bytes [0, min(decoded, cap)) decoded, the rest
+// of the slot zeroed, so a short text never leaves stale device bytes in the
+// caller's slot.  sizes[i] = min(decoded, cap[i]), over[i] = decoded > cap[i].
 __global__ void __launch_bounds__(kB64Threads) b64_decode_canon_kernel(const uint8_t* __restrict__ text,
                                                                        const uint64_t* __restrict__ text_off,
                                                                        const uint32_t* __restrict__ text_len,
@@ -117,69 +187,80 @@ __global__ void __launch_bounds__(kB64Threads) b64_decode_canon_kernel(const uin
                                                                        const uint32_t* __restrict__ cap,
                                                                        uint32_t* __restrict__ sizes,
                                                                        uint8_t* __restrict__ over,
-                                                                       uint8_t* __restrict__ redo) {
+                                                                       uint8_t* __restrict__ redo, uint32_t tiles,
+                                                                       uint32_t chunk0) {
+  constexpr uint32_t kStage = (kB64TileText + 15 + 15) / 16 + 1;  // the span, its phase, one block of slack
+  __shared__ uint4 stage[kStage];
   __shared__ uint8_t tab[256];
-  tab[threadIdx.x] = g_b64_table.v[threadIdx.x];
-  __syncthreads();
-  const uint32_t i = blockIdx.x, part = blockIdx.y, parts = gridDim.y;
-  const uint8_t* t = text + text_off[i];
+  const uint32_t i = chunk0 + blockIdx.x / tiles, tile = blockIdx.x % tiles;
   const uint32_t len = text_len[i];
   uint32_t groups = 0;
-  if (!b64_canon_groups(len, &groups)) {
-    if (part == 0 && threadIdx.x == 0) redo[i] = 1;
+  if (!b64_canon_groups(len, &groups)) {  // the whole workgroup leaves: no barrier below is reached
+    if (tile == 0 && threadIdx.x == 0) redo[i] = 1;
     return;
   }
   const uint32_t limit = cap[i];
-  uint8_t* o = out + out_off[i];
-  // the last group: "xxxx", "xxx=" or "xx=="; its byte count sets the length
+  const uint32_t tbeg = tile * kB64TileText, obeg = tile * kB64TileBytes;
+  const uint8_t* t = text + text_off[i];
+  // the last group: "xxxx", "xxx=" or "xx==" sets the decoded length
   uint32_t last = 3;
   bool bad = false;
   if (groups > 0) {
     const uint32_t g = groups - 1, at = 4 * g + g / 18;
-    const uint8_t c2 = tab[t[at + 2]], c3 = tab[t[at + 3]];
+    const uint8_t c2 = g_b64_table.v[t[at + 2]], c3 = g_b64_table.v[t[at + 3]];
     last = c3 < 64 ? 3u : c2 < 64 ? 2u : 1u;
     bad = c3 == kB64Skip || c2 == kB64Skip || (c2 == kB64Eq && c3 != kB64Eq);
   }
   const uint64_t want = groups ? 3ull * (groups - 1) + last : 0;
-  if (part == 0 && threadIdx.x == 0) {
+  if (tile == 0 && threadIdx.x == 0) {
     sizes[i] = (uint32_t)min<uint64_t>(want, limit);
     over[i] = want > limit ? 1 : 0;
+    if (bad) redo[i] = 1;
   }
-  const uint32_t tasks = (groups + 3) / 4;
-  const uint32_t per = (tasks + parts - 1) / parts;
-  const uint32_t end = min(tasks, (part + 1) * per);
-  for (uint32_t k = part * per + threadIdx.x; k < end; k += kB64Threads) {
-    uint8_t b[12];
-    uint32_t nb = 0;
+  if (tbeg >= len && obeg >= limit) return;  // a tile past this chunk's text and slot (the whole workgroup)
+  tab[threadIdx.x] = g_b64_table.v[threadIdx.x];
+  const uint32_t delta = tbeg < len ? b64_stage_span<kStage>(t + tbeg, min(kB64TileText, len - tbeg), stage) : 0u;
+  __syncthreads();
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(stage);
+  const uint8_t* sb = reinterpret_cast<const uint8_t*>(stage);
+  if (threadIdx.x < kB64TileBytes / 16) {
+    // bytes [16u, 16u + 16) of the tile come from its groups g0 .. g0 + 5
+    const uint32_t b0 = 16 * threadIdx.x, g0 = b0 / 3, phase = b0 - 3 * g0;
+    uint32_t x[6];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint32_t g = 4 * k + j;
-      if (g >= groups) break;
-      const uint32_t at = 4 * g + g / 18;
-      const uint8_t v0 = tab[t[at]], v1 = tab[t[at + 1]], v2 = tab[t[at + 2]], v3 = tab[t[at + 3]];
-      if (g + 1 < groups) {
-        bad |= (v0 | v1 | v2 | v3) >= 64;  // '=' (64) or skip (255) inside the text
-        if (g % 18 == 17) bad |= tab[t[at + 4]] != kB64Skip;  // the separator
-      } else {
-        bad |= v0 >= 64 || v1 >= 64;  // the last group's padding was checked above
-        if (g % 18 == 17) bad |= tab[t[at + 4]] != kB64Skip;
+    for (int j = 0; j < 6; ++j) {
+      const uint32_t gl = g0 + j, gg = tile * kB64TileGroups + gl;
+      x[j] = 0;
+      if (gg < groups) {
+        const uint32_t at = delta + 4 * gl + gl / 18;
+        const uint32_t c = lds_u32_at(w, at);
+        const uint32_t s0 = tab[c & 255], s1 = tab[(c >> 8) & 255], s2 = tab[(c >> 16) & 255], s3 = tab[c >> 24];
+        // inside the text every character is in the alphabet; the last
+        // group's padding was checked above
+        bad |= gg + 1 < groups ? (s0 | s1 | s2 | s3) >= 64 : (s0 | s1) >= 64;
+        if (gl % 18 == 17 && 4 * gg + gg / 18 + 4 < len) bad |= tab[sb[at + 4]] != kB64Skip;  // the separator
+        x[j] = ((s0 & 63) << 18) | ((s1 & 63) << 12) | ((s2 & 63) << 6) | (s3 & 63);
       }
-      const uint32_t x = ((uint32_t)(v0 & 63) << 18) | ((uint32_t)(v1 & 63) << 12) | ((uint32_t)(v2 & 63) << 6) |
-                         (v3 & 63);
-      b[3 * j] = (uint8_t)(x >> 16);
-      b[3 * j + 1] = (uint8_t)(x >> 8);
-      b[3 * j + 2] = (uint8_t)x;
-      nb = g + 1 < groups ? nb + 3 : nb + last;
     }
-    const uint64_t at = 12ull * k;
-    if (nb == 12 && at + 12 <= limit && (reinterpret_cast<uintptr_t>(o + at) & 3u) == 0) {
-      uint32_t* d = reinterpret_cast<uint32_t*>(o + at);
+    // the 18 bytes of the six groups, as little-endian words
+    auto by = [&](int j, int k) { return (x[j] >> (16 - 8 * k)) & 255u; };
+    const uint32_t W0 = by(0, 0) | by(0, 1) << 8 | by(0, 2) << 16 | by(1, 0) << 24;
+    const uint32_t W1 = by(1, 1) | by(1, 2) << 8 | by(2, 0) << 16 | by(2, 1) << 24;
+    const uint32_t W2 = by(2, 2) | by(3, 0) << 8 | by(3, 1) << 16 | by(3, 2) << 24;
+    const uint32_t W3 = by(4, 0) | by(4, 1) << 8 | by(4, 2) << 16 | by(5, 0) << 24;
+    const uint32_t W4 = by(5, 1) | by(5, 2) << 8;
+    uint4 v = make_uint4(__builtin_amdgcn_alignbyte(W1, W0, phase), __builtin_amdgcn_alignbyte(W2, W1, phase),
+                         __builtin_amdgcn_alignbyte(W3, W2, phase), __builtin_amdgcn_alignbyte(W4, W3, phase));
+    const uint64_t pos = obeg + b0;
+    if (pos < limit) {
+      if (pos + 16 > want) {  // the decoded bytes end inside this block: zero the rest of the slot
+        uint32_t ws[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-      for (int j = 0; j < 3; ++j)
-        d[j] = (uint32_t)b[4 * j] | ((uint32_t)b[4 * j + 1] << 8) | ((uint32_t)b[4 * j + 2] << 16) |
-               ((uint32_t)b[4 * j + 3] << 24);
-    } else {
-      for (uint32_t j = 0; j < nb && at + j < limit; ++j) o[at + j] = b[j];
+        for (int m = 0; m < 16; ++m)
+          if (pos + m >= want) ws[m >> 2] &= ~(255u << (8 * (m & 3)));
+        v = make_uint4(ws[0], ws[1], ws[2], ws[3]);
+      }
+      b64_put_block(out + out_off[i], pos, limit, v);
     }
   }
   if (bad) redo[i] = 1;  // every writer stores the same 1
@@ -313,6 +394,8 @@ __global__ void __launch_bounds__(kB64Threads) b64_decode_kernel(const uint8_t* 
     sizes[i] = (uint32_t)min<uint64_t>(want, limit);
     over[i] = want > limit ? 1 : 0;
   }
+  // the rest of the slot: zeros, never stale device bytes (lbf_b64_verify_batch copies whole slots back)
+  for (uint64_t p = want + threadIdx.x; p < limit; p += kB64Threads) o[p] = 0;
 }
 
 }  // namespace
@@ -335,37 +418,69 @@ __host__ __device__ constexpr uint64_t b64_put_length(uint64_t size) {
   return 4 * (size / 3) + (size % 3 ? 4 : 0) + size / 3 / 18;
 }
 
+// blockIdx.x = (chunk - chunk0) * tiles + tile: tile k of chunk i encodes bytes
+// [3456k, +3456) into text [4672k, +4672) (clipped to the chunk).  Each lane
+// writes one 16-byte block of the text: characters [p, p + 16) of a line lie
+// in at most five consecutive "words" of the line's character stream, where
+// word e of line l is group e's four characters for e < 18 and, past the
+// line's end, the next line's group e - 18 shifted one byte right behind the
+// separator; v_alignbyte cuts the block out of them.
 __global__ void __launch_bounds__(kB64Threads) b64_encode_kernel(const uint8_t* __restrict__ data,
                                                                  const uint64_t* __restrict__ data_off,
                                                                  const uint32_t* __restrict__ size,
                                                                  uint8_t* __restrict__ text,
-                                                                 const uint64_t* __restrict__ text_off) {
+                                                                 const uint64_t* __restrict__ text_off, uint32_t tiles,
+                                                                 uint32_t chunk0) {
+  // the span, its phase, and slack for the group reads of the last window
+  // (computed for every word, used only inside the tile)
+  constexpr uint32_t kStage = (kB64TileBytes + 15) / 16 + 4;
+  __shared__ uint4 stage[kStage];
   __shared__ uint8_t alpha[64];
+  const uint32_t i = chunk0 + blockIdx.x / tiles, tile = blockIdx.x % tiles;
+  const uint32_t n = size[i], full = n / 3, rest = n % 3;
+  const uint64_t tl = b64_put_length(n);
+  const uint32_t tbeg = tile * kB64TileText, dbeg = tile * kB64TileBytes;
+  if (tbeg >= tl) return;  // the whole workgroup: no barrier below is reached
   if (threadIdx.x < 64) {
     const uint32_t c = threadIdx.x;
     alpha[c] = (uint8_t)(c < 26 ? 'A' + c : c < 52 ? 'a' + (c - 26) : c < 62 ? '0' + (c - 52) : c == 62 ? '+' : '/');
   }
+  const uint32_t delta =
+      dbeg < n ? b64_stage_span<kStage>(data + data_off[i] + dbeg, min(kB64TileBytes, n - dbeg), stage) : 0u;
   __syncthreads();
-  const uint32_t i = blockIdx.x;
-  const uint8_t* d = data + data_off[i];
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(stage);
   uint8_t* t = text + text_off[i];
-  const uint32_t n = size[i], full = n / 3;
-  for (uint32_t g = threadIdx.x; g < full; g += kB64Threads) {
-    const uint32_t x = ((uint32_t)d[3 * g] << 16) | ((uint32_t)d[3 * g + 1] << 8) | d[3 * g + 2];
-    uint8_t* o = t + 4ull * g + g / 18;
-    o[0] = alpha[x >> 18];
-    o[1] = alpha[(x >> 12) & 63];
-    o[2] = alpha[(x >> 6) & 63];
-    o[3] = alpha[x & 63];
-    if (g % 18 == 17) o[4] = ' ';  // base64.h:197-205's newline, framed as a space
-  }
-  if (threadIdx.x == 0 && n % 3) {
-    uint8_t* o = t + 4ull * full + full / 18;
-    const uint32_t x = ((uint32_t)d[3 * full] << 16) | (n % 3 == 2 ? (uint32_t)d[3 * full + 1] << 8 : 0u);
-    o[0] = alpha[x >> 18];
-    o[1] = alpha[(x >> 12) & 63];
-    o[2] = n % 3 == 2 ? alpha[(x >> 6) & 63] : (uint8_t)'=';
-    o[3] = '=';
+  // group gl of the tile as its four characters, first character in the low byte
+  auto chars = [&](uint32_t gl) -> uint32_t {
+    const uint32_t gg = tile * kB64TileGroups + gl;
+    if (gg > full || (gg == full && rest == 0)) return 0u;  // past the text
+    const uint32_t b = lds_u32_at(w, delta + 3 * gl);
+    uint32_t x = (b & 255u) << 16 | ((b >> 8) & 255u) << 8 | ((b >> 16) & 255u);
+    if (gg < full)
+      return (uint32_t)alpha[x >> 18] | (uint32_t)alpha[(x >> 12) & 63] << 8 | (uint32_t)alpha[(x >> 6) & 63] << 16 |
+             (uint32_t)alpha[x & 63] << 24;
+    x &= rest == 2 ? 0xFFFF00u : 0xFF0000u;  // the last one or two bytes: "xxx=" / "xx=="
+    return (uint32_t)alpha[x >> 18] | (uint32_t)alpha[(x >> 12) & 63] << 8 |
+           (rest == 2 ? (uint32_t)alpha[(x >> 6) & 63] : (uint32_t)'=') << 16 | (uint32_t)'=' << 24;
+  };
+  for (uint32_t v = threadIdx.x; v < kB64TileText / 16; v += kB64Threads) {
+    const uint32_t p0 = 16 * v;
+    const uint64_t pos = tbeg + p0;
+    if (pos >= tl) break;
+    const uint32_t line = p0 / 73, col = p0 - 73 * line, e0 = col >> 2;
+    uint32_t g[5], E[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) g[k] = chars(18 * line + e0 + k);
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      const uint32_t e = e0 + k;
+      // past the line's 18 groups: the separator, then the next line's characters one byte right
+      E[k] = e <= 17 ? g[k] : (g[k] << 8) | (e == 18 ? (uint32_t)' ' : (k > 0 ? g[k - 1] >> 24 : 0u));
+    }
+    const uint32_t sh = col & 3;
+    const uint4 out = make_uint4(__builtin_amdgcn_alignbyte(E[1], E[0], sh), __builtin_amdgcn_alignbyte(E[2], E[1], sh),
+                                 __builtin_amdgcn_alignbyte(E[3], E[2], sh), __builtin_amdgcn_alignbyte(E[4], E[3], sh));
+    b64_put_block(t, pos, tl, out);
   }
 }
 

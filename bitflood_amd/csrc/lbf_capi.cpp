@@ -491,6 +491,8 @@ struct lbf_ctx {
   // worker 0's device: one allocation, grown on demand, guarded by mu
   uint8_t* b64_dev = nullptr;
   uint64_t b64_cap = 0;
+  // lbf_b64_verify_batch's chunks by decode path (lbf_ctx_b64_stats), guarded by mu
+  uint64_t b64_one_pass = 0, b64_general = 0;
   mutable std::mutex mu;
 };
 
@@ -1371,6 +1373,14 @@ extern "C" int lbf_ctx_num_devices(const lbf_ctx* ctx) {
 
 extern "C" int lbf_ctx_num_workers(const lbf_ctx* ctx) { return ctx ? (int)ctx->workers.size() : 0; }
 
+extern "C" int lbf_ctx_b64_stats(lbf_ctx* ctx, uint64_t* one_pass_chunks, uint64_t* general_chunks) {
+  if (!ctx) return fail(LBF_ERR_INVALID, "null context");
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  if (one_pass_chunks) *one_pass_chunks = ctx->b64_one_pass;
+  if (general_chunks) *general_chunks = ctx->b64_general;
+  return LBF_OK;
+}
+
 extern "C" int lbf_ctx_staging_stats(lbf_ctx* ctx, uint64_t* staged_bytes, uint64_t* direct_bytes) {
   if (!ctx) return fail(LBF_ERR_INVALID, "null context");
   std::lock_guard<std::mutex> lock(ctx->mu);  // between jobs
@@ -1413,14 +1423,21 @@ extern "C" int lbf_host_register(lbf_ctx* ctx, const void* ptr, uint64_t len) {
       return fail(LBF_ERR_INVALID, "lbf_host_register: range overlaps, but differs from, one another context holds");
     // Pinned already by someone else (a hipHostMalloc'd buffer, a caller's own
     // registration): use it, never unpin it -- but only if ONE pinned
-    // allocation covers the whole range.  Its first and last page being pinned
-    // is not enough: they may belong to two neighbouring allocations with
-    // pageable memory between them, which a direct copy would then read.
-    const PinnedAlloc first = pinned_alloc(r.lo), last = pinned_alloc(r.hi - page);
-    if (first.pinned && first.base <= r.lo && r.hi <= first.end) {
+    // allocation covers the caller's whole range.  Its first and last byte
+    // being pinned is not enough: they may belong to two neighbouring
+    // allocations with pageable memory between them, which a direct copy would
+    // then read.  The caller's bytes [a, a + len) are what is checked (a
+    // buffer pinned whole by the caller need not end on a page boundary).
+    const uint64_t uend = a + len;
+    const PinnedAlloc first = pinned_alloc(a), last = pinned_alloc(uend - 1);
+    if (first.pinned && first.end && first.base <= a && uend <= first.end) {
       ctx->regs.push_back(r);
       return (int)LBF_OK;
     }
+    if (first.pinned && !first.end)
+      return fail(LBF_ERR_INVALID,
+                  "lbf_host_register: range is pinned already, but HIP does not report the extent of the pinned "
+                  "allocation holding it, so it cannot be shown to cover the range");
     if (first.pinned || last.pinned)
       return fail(LBF_ERR_INVALID,
                   "lbf_host_register: range is partly pinned already (no single pinned allocation holds all of it)");
@@ -1622,6 +1639,44 @@ int b64_scratch(lbf_ctx* ctx, uint64_t need, const char* who) {
   ctx->b64_cap = want;
   return LBF_OK;
 }
+
+// Every exit of a base64 entry point after its first async copy waits for the
+// stream, so no copy is still reading a local staging vector or the caller's
+// (possibly pinned) buffers, or writing into them, once the call has returned
+// (ADVICE r04).  Declared after the host vectors the copies use, so it runs
+// before they are destroyed.
+struct SyncOnExit {
+  hipStream_t st;
+  ~SyncOnExit() {
+    (void)hipStreamSynchronize(st);
+    (void)hipGetLastError();
+  }
+};
+
+// Caller slots [off[i], off[i] + len[i]) that the device writes back: sorted,
+// checked for overlap (two chunks' results in one byte would race on the
+// device), and merged into runs of touching slots.  Each run is one D2H; the
+// bytes between runs are the caller's and are never written.
+struct SlotRun {
+  uint64_t lo, hi;
+};
+int slot_runs(const uint64_t* off, const uint64_t* len, uint64_t n, const char* who, std::vector<SlotRun>& runs) {
+  std::vector<uint64_t> idx;
+  idx.reserve(n);
+  for (uint64_t i = 0; i < n; ++i)
+    if (len[i]) idx.push_back(i);
+  std::sort(idx.begin(), idx.end(), [&](uint64_t a, uint64_t b) { return off[a] < off[b]; });
+  runs.clear();
+  for (uint64_t i : idx) {
+    if (!runs.empty() && off[i] < runs.back().hi)
+      return fail(LBF_ERR_INVALID, std::string(who) + ": slot " + std::to_string(i) + " overlaps another slot");
+    if (!runs.empty() && off[i] == runs.back().hi)
+      runs.back().hi += len[i];
+    else
+      runs.push_back(SlotRun{off[i], off[i] + len[i]});
+  }
+  return LBF_OK;
+}
 }  // namespace
 
 extern "C" uint64_t lbf_b64_put_length(uint64_t size) { return 4 * (size / 3) + (size % 3 ? 4 : 0) + size / 3 / 18; }
@@ -1653,8 +1708,13 @@ extern "C" int lbf_verify_encode_b64_batch(lbf_ctx* ctx, const uint8_t* data, ui
     tlo = std::min(tlo, text_offsets[i]);
     thi = std::max(thi, text_offsets[i] + tl);
   }
-  const uint64_t text_first = tlo;  // the D2H starts here: no byte before the lowest slot is written
-  dlo &= ~15ull;                    // device offsets keep the host offsets' alignment mod 16
+  uint32_t max_size = 0;
+  for (uint64_t i = 0; i < n; ++i) max_size = std::max(max_size, sizes[i]);
+  std::vector<uint64_t> tlens(n);
+  for (uint64_t i = 0; i < n; ++i) tlens[i] = lbf_b64_put_length(sizes[i]);
+  std::vector<SlotRun> runs;  // the text slots the D2H writes, and nothing between them
+  if (int rc = slot_runs(text_offsets, tlens.data(), n, "lbf_verify_encode_b64_batch", runs)) return rc;
+  dlo &= ~15ull;  // device offsets keep the host offsets' alignment mod 16
   tlo &= ~15ull;
   return guarded([&] {
     auto up = [](uint64_t x, uint64_t a) { return (x + a - 1) / a * a; };
@@ -1681,6 +1741,7 @@ extern "C" int lbf_verify_encode_b64_batch(lbf_ctx* ctx, const uint8_t* data, ui
     uint8_t* d_in = d_text + text_b;
     uint8_t* d_ver = d_in + in_b;
     hipStream_t st = w.dev[0].stream;
+    SyncOnExit sync{st};
     if (dhi > dlo) LBF_HIP_TRY(hipMemcpyAsync(d_data, data + dlo, dhi - dlo, hipMemcpyHostToDevice, st));
     LBF_HIP_TRY(hipMemcpyAsync(d_in, in.data(), in.size(), hipMemcpyHostToDevice, st));
     const uint64_t* d_doff = reinterpret_cast<const uint64_t*>(d_in);
@@ -1688,11 +1749,10 @@ extern "C" int lbf_verify_encode_b64_batch(lbf_ctx* ctx, const uint8_t* data, ui
     const uint32_t* d_sz = reinterpret_cast<const uint32_t*>(d_toff + n);
     const uint8_t* d_exp = reinterpret_cast<const uint8_t*>(d_sz + n);
     if (int rc = lbf_sha1_launch(d_data, d_doff, d_sz, n, nullptr, d_exp, d_ver, st)) return rc;
-    if (int rc = lbf::launch_b64_encode(d_data, d_doff, d_sz, d_text, d_toff, (uint32_t)n, st)) return rc;
+    if (int rc = lbf::launch_b64_encode(d_data, d_doff, d_sz, d_text, d_toff, (uint32_t)n, max_size, st)) return rc;
     LBF_HIP_TRY(hipMemcpyAsync(verdicts, d_ver, n, hipMemcpyDeviceToHost, st));
-    if (thi > text_first)
-      LBF_HIP_TRY(hipMemcpyAsync(text + text_first, d_text + (text_first - tlo), thi - text_first, hipMemcpyDeviceToHost,
-                                 st));
+    for (const SlotRun& r : runs)
+      LBF_HIP_TRY(hipMemcpyAsync(text + r.lo, d_text + (r.lo - tlo), r.hi - r.lo, hipMemcpyDeviceToHost, st));
     LBF_HIP_TRY(hipStreamSynchronize(st));
     return (int)LBF_OK;
   });
@@ -1726,9 +1786,18 @@ extern "C" int lbf_b64_verify_batch(lbf_ctx* ctx, const char* text, uint64_t tex
       ohi = std::max(ohi, out_offsets[i] + expected_sizes[i]);
     }
   }
-  // device offsets keep the host offsets' alignment mod 16; the D2H starts at
-  // the lowest slot itself (out_first), so no byte before it is written
-  const uint64_t out_first = olo;
+  // device offsets keep the host offsets' alignment mod 16; the D2H writes the
+  // output slots and nothing between them
+  std::vector<SlotRun> runs;
+  if (out) {
+    std::vector<uint64_t> olens(expected_sizes, expected_sizes + n);
+    if (int rc = slot_runs(out_offsets, olens.data(), n, "lbf_b64_verify_batch", runs)) return rc;
+  }
+  uint32_t max_tlen = 0, max_cap = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    max_tlen = std::max(max_tlen, text_lens[i]);
+    max_cap = std::max(max_cap, expected_sizes[i]);
+  }
   tlo &= ~15ull;
   if (out) olo &= ~15ull;
   return guarded([&] {
@@ -1750,11 +1819,13 @@ extern "C" int lbf_b64_verify_batch(lbf_ctx* ctx, const char* text, uint64_t tex
       }
     }
     if (out) outb = ohi - olo;
-    // device layout: text | sextets | bytes | inputs (offsets, lengths, caps, expected, zeroed redo flags) |
-    // outputs (sizes, over, verdicts)
+    // device layout: text | sextets | bytes | inputs (offsets, lengths, caps, expected) then, right behind
+    // them, the results (sizes, over, verdicts, redo flags): one H2D carries the inputs and the zeroed
+    // results, one D2H brings the results back
+    const uint64_t kIn = 8 * 3 + 4 * 2 + 20, kRes = 4 + 1 + 1 + 1;  // bytes per chunk; kIn * n keeps 4-byte alignment
     const uint64_t text_b = up(thi - tlo, 256), sext_b = up(sext, 256), out_b = up(outb + 16, 256);
-    const uint64_t in_b = up(n * (8 * 3 + 4 * 2 + 20 + 1), 256), res_b = up(n * (4 + 1 + 1), 256);
-    const uint64_t need = text_b + sext_b + out_b + in_b + res_b;
+    const uint64_t io_b = up(n * (kIn + kRes), 256);
+    const uint64_t need = text_b + sext_b + out_b + io_b;
     std::lock_guard<std::mutex> lock(ctx->mu);
     KeepCurrentDevice keep;
     Worker& w = ctx->workers[0];
@@ -1764,8 +1835,8 @@ extern "C" int lbf_b64_verify_batch(lbf_ctx* ctx, const char* text, uint64_t tex
     uint8_t* d_sext = d_text + text_b;
     uint8_t* d_out = d_sext + sext_b;
     uint8_t* d_in = d_out + out_b;
-    uint8_t* d_res = d_in + in_b;
-    std::vector<uint8_t> in(n * (8 * 3 + 4 * 2 + 20 + 1), 0);
+    uint8_t* d_res = d_in + kIn * n;
+    std::vector<uint8_t> in(n * (kIn + kRes), 0);
     uint8_t* q = in.data();
     auto put = [&](const void* src, uint64_t bytes) {
       memcpy(q, src, bytes);
@@ -1778,6 +1849,8 @@ extern "C" int lbf_b64_verify_batch(lbf_ctx* ctx, const char* text, uint64_t tex
     put(cap.data(), 4 * n);
     put(expected, 20 * n);
     hipStream_t st = w.dev[0].stream;
+    std::vector<uint8_t> res(n * kRes);
+    SyncOnExit sync{st};
     if (thi > tlo) LBF_HIP_TRY(hipMemcpyAsync(d_text, text + tlo, thi - tlo, hipMemcpyHostToDevice, st));
     LBF_HIP_TRY(hipMemcpyAsync(d_in, in.data(), in.size(), hipMemcpyHostToDevice, st));
     const uint64_t* d_toff = reinterpret_cast<const uint64_t*>(d_in);
@@ -1786,19 +1859,24 @@ extern "C" int lbf_b64_verify_batch(lbf_ctx* ctx, const char* text, uint64_t tex
     const uint32_t* d_tlen = reinterpret_cast<const uint32_t*>(d_ooff + n);
     const uint32_t* d_cap = d_tlen + n;
     const uint8_t* d_exp = reinterpret_cast<const uint8_t*>(d_cap + n);
-    uint8_t* d_redo = const_cast<uint8_t*>(d_exp) + 20 * n;  // uploaded as zeros
     uint32_t* d_sizes = reinterpret_cast<uint32_t*>(d_res);
     uint8_t* d_over = reinterpret_cast<uint8_t*>(d_sizes + n);
     uint8_t* d_ver = d_over + n;
-    lbf::B64Launch b{d_text, d_sext, d_toff, d_soff, d_tlen, d_out, d_ooff, d_cap, d_sizes, d_over, d_redo, (uint32_t)n};
+    uint8_t* d_redo = d_ver + n;  // uploaded as zeros
+    lbf::B64Launch b{d_text, d_sext, d_toff, d_soff, d_tlen, d_out,   d_ooff, d_cap,
+                     d_sizes, d_over, d_redo, (uint32_t)n, max_tlen, max_cap};
     if (int rc = lbf::launch_b64_decode(b, st)) return rc;
     // the decoded lengths are the chunk sizes the hash kernels read
     if (int rc = lbf_sha1_launch(d_out, d_ooff, d_sizes, n, nullptr, d_exp, d_ver, st)) return rc;
-    std::vector<uint8_t> res(n * 6);
     LBF_HIP_TRY(hipMemcpyAsync(res.data(), d_res, res.size(), hipMemcpyDeviceToHost, st));
-    if (out && ohi > out_first)
-      LBF_HIP_TRY(hipMemcpyAsync(out + out_first, d_out + (out_first - olo), ohi - out_first, hipMemcpyDeviceToHost, st));
+    for (const SlotRun& r : runs)
+      LBF_HIP_TRY(hipMemcpyAsync(out + r.lo, d_out + (r.lo - olo), r.hi - r.lo, hipMemcpyDeviceToHost, st));
     LBF_HIP_TRY(hipStreamSynchronize(st));
+    const uint8_t* redo = res.data() + 6 * n;
+    uint64_t general = 0;
+    for (uint64_t i = 0; i < n; ++i) general += redo[i] != 0;
+    ctx->b64_general += general;
+    ctx->b64_one_pass += n - general;
     const uint32_t* sizes = reinterpret_cast<const uint32_t*>(res.data());
     const uint8_t* over = res.data() + 4 * n;
     const uint8_t* ver = over + n;

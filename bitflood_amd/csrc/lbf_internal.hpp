@@ -52,11 +52,14 @@ struct B64Launch {
   uint8_t* over;
   uint8_t* redo;  // n bytes, zero on entry: the chunks the one-pass decode hands to the general one
   uint32_t n;
+  uint32_t max_text_len;  // the longest text and the largest cap: the one-pass decode's tiles per chunk
+  uint32_t max_cap;
 };
 int launch_b64_decode(const B64Launch& b, hipStream_t stream);
 // Device base64 encode (kern_b64.hpp): n chunks' bytes -> their SendChunk text.
+// max_size: the largest chunk (sets the tiles per chunk).
 int launch_b64_encode(const uint8_t* data, const uint64_t* data_off, const uint32_t* size, uint8_t* text,
-                      const uint64_t* text_off, uint32_t n, hipStream_t stream);
+                      const uint64_t* text_off, uint32_t n, uint32_t max_size, hipStream_t stream);
 
 // Kernel variants beyond the shipped ones (1, 7, 10, 11, 12).  Null in the
 // shipped library; the A/B library of tools/experimental/ points it at its

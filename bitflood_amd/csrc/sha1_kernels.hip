@@ -179,15 +179,31 @@ int launch_chunks(const ChunkParams& p, hipStream_t stream) {
   return LBF_OK;
 }
 
+// grid.x = chunks x tiles, in launches of at most 2^22 workgroups (a chunk's
+// tiles are never split across launches)
+template <class F>
+static int b64_tiled_launch(uint32_t n, uint32_t tiles, F launch) {
+  const uint32_t per = std::max(1u, (1u << 22) / tiles);
+  for (uint32_t c0 = 0; c0 < n; c0 += per) {
+    launch(dim3(std::min(per, n - c0) * tiles), c0);
+    LBF_HIP_TRY(hipGetLastError());
+  }
+  return LBF_OK;
+}
+
 int launch_b64_decode(const B64Launch& b, hipStream_t stream) {
   if (b.n == 0) return LBF_OK;
-  // the one-pass decode of canonically laid-out text, split over enough
-  // workgroups to fill the chip at small batches; then the general two-pass
-  // decode of whatever it handed back (a workgroup per chunk, most exit at once)
-  const uint32_t parts = std::max(1u, std::min(16u, 2048u / b.n));
-  hipLaunchKernelGGL(b64_decode_canon_kernel, dim3(b.n, parts), dim3(kB64Threads), 0, stream, b.text, b.text_off,
-                     b.text_len, b.out, b.out_off, b.cap, b.sizes, b.over, b.redo);
-  LBF_HIP_TRY(hipGetLastError());
+  // the one-pass decode of canonically laid-out text, tile by tile (each
+  // chunk's tiles cover its text and its output slot); then the general
+  // two-pass decode of whatever it handed back (a workgroup per chunk, most
+  // exit at once)
+  const uint32_t tiles = std::max<uint32_t>(
+      1u, std::max((b.max_text_len + kB64TileText - 1) / kB64TileText, (b.max_cap + kB64TileBytes - 1) / kB64TileBytes));
+  if (int rc = b64_tiled_launch(b.n, tiles, [&](dim3 grid, uint32_t c0) {
+        hipLaunchKernelGGL(b64_decode_canon_kernel, grid, dim3(kB64Threads), 0, stream, b.text, b.text_off, b.text_len,
+                           b.out, b.out_off, b.cap, b.sizes, b.over, b.redo, tiles, c0);
+      }))
+    return rc;
   hipLaunchKernelGGL(b64_decode_kernel, dim3(b.n), dim3(kB64Threads), 0, stream, b.text, b.scratch, b.text_off,
                      b.sext_off, b.text_len, b.out, b.out_off, b.cap, b.sizes, b.over, (const uint8_t*)b.redo);
   LBF_HIP_TRY(hipGetLastError());
@@ -195,11 +211,13 @@ int launch_b64_decode(const B64Launch& b, hipStream_t stream) {
 }
 
 int launch_b64_encode(const uint8_t* data, const uint64_t* data_off, const uint32_t* size, uint8_t* text,
-                      const uint64_t* text_off, uint32_t n, hipStream_t stream) {
+                      const uint64_t* text_off, uint32_t n, uint32_t max_size, hipStream_t stream) {
   if (n == 0) return LBF_OK;
-  hipLaunchKernelGGL(b64_encode_kernel, dim3(n), dim3(kB64Threads), 0, stream, data, data_off, size, text, text_off);
-  LBF_HIP_TRY(hipGetLastError());
-  return LBF_OK;
+  const uint32_t tiles = std::max<uint32_t>(1u, (uint32_t)((b64_put_length(max_size) + kB64TileText - 1) / kB64TileText));
+  return b64_tiled_launch(n, tiles, [&](dim3 grid, uint32_t c0) {
+    hipLaunchKernelGGL(b64_encode_kernel, grid, dim3(kB64Threads), 0, stream, data, data_off, size, text, text_off, tiles,
+                       c0);
+  });
 }
 
 }  // namespace lbf

@@ -105,6 +105,14 @@ class ChunkHasher:
         check(self._lib.lbf_ctx_staging_stats(self._h, ctypes.byref(st), ctypes.byref(di)))
         return {"staged": st.value, "direct": di.value}
 
+    def b64_stats(self) -> dict:
+        """Chunks of verify_b64 calls so far by decode path: text with the
+        encoder's own layout decoded in one pass, the rest by the general
+        two-pass kernel (lbf_ctx_b64_stats)."""
+        one, gen = ctypes.c_uint64(0), ctypes.c_uint64(0)
+        check(self._lib.lbf_ctx_b64_stats(self._h, ctypes.byref(one), ctypes.byref(gen)))
+        return {"one_pass": one.value, "general": gen.value}
+
     # -- caller-pinned sources (lbf_host_register) ---------------------------
     def register_host(self, data) -> None:
         """Pin `data` (a contiguous numpy array / buffer) for this context:

@@ -160,11 +160,13 @@ int lbf_files_ranges(lbf_ctx* ctx, const char* const* paths, uint32_t n_files, c
  * expected[20*i .. 20*i+20).  out_sizes[i] (may be NULL) receives the decoded
  * length, or expected_sizes[i] + 1 when the text decodes to more.  With `out`
  * non-NULL the decoded bytes land at out[out_offsets[i], + expected_sizes[i])
- * (host memory, slots must not overlap); bytes of `out` between the lowest
- * slot and the end of the highest that are not decoded bytes are unspecified
- * afterwards; bytes outside that span are not written.  Synchronous, on the
- * context's first device.  Text and output
- * in memory registered with lbf_host_register move by DMA without staging. */
+ * (host memory); the bytes of a slot past its decoded length are zeroed,
+ * and no byte of `out` outside the slots is written.  Overlapping slots are
+ * refused (LBF_ERR_INVALID).  Synchronous, on the context's first device.
+ * Text and output in memory registered with lbf_host_register move by DMA
+ * without staging.  lbf_ctx_b64_stats counts the chunks whose text had the
+ * encoder's own layout (decoded in one pass) and the others (decoded by the
+ * general two-pass kernel). */
 int lbf_b64_verify_batch(lbf_ctx* ctx, const char* text, uint64_t text_len, const uint64_t* text_offsets,
                          const uint32_t* text_lens, uint64_t n, const uint32_t* expected_sizes,
                          const uint8_t* expected, uint8_t* out, uint64_t out_len, const uint64_t* out_offsets,
@@ -179,13 +181,15 @@ int lbf_b64_verify_batch(lbf_ctx* ctx, const char* text, uint64_t text_len, cons
  * its text -- four characters per three bytes, a space (the frame's newline)
  * after every 18th complete group, "xx==" / "xxx=" for a last one or two
  * bytes -- lands at text[text_offsets[i], + lbf_b64_put_length(sizes[i]))
- * whatever the verdict (slots must not overlap).  Bytes of `text` between the
- * lowest slot and the end of the highest that are not written text are
- * unspecified afterwards; bytes outside that span are not written.
- * Synchronous, on the context's first device. */
+ * whatever the verdict; no byte of `text` outside the slots is written, and
+ * overlapping slots are refused (LBF_ERR_INVALID).  Synchronous, on the
+ * context's first device. */
 int lbf_verify_encode_b64_batch(lbf_ctx* ctx, const uint8_t* data, uint64_t data_len, const uint64_t* offsets,
                                 const uint32_t* sizes, uint64_t n, const uint8_t* expected, uint8_t* verdicts,
                                 char* text, uint64_t text_len, const uint64_t* text_offsets);
+/* Chunks of lbf_b64_verify_batch calls on this context so far, by decode
+ * path (diagnostics; either pointer may be NULL). */
+int lbf_ctx_b64_stats(lbf_ctx* ctx, uint64_t* one_pass_chunks, uint64_t* general_chunks);
 /* Length of that text for a chunk of `size` bytes (xmlrpc++'s encoder). */
 uint64_t lbf_b64_put_length(uint64_t size);
 

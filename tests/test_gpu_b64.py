@@ -212,9 +212,10 @@ def test_sender_encode_matches_xmlrpc_text(hasher):
 
 
 def test_outputs_touch_nothing_outside_their_slots(hasher):
-    """Both entry points copy results back from the lowest slot on: the bytes
-    of `out` / `text` before the first slot and after the last stay as they
-    were, whatever the slots' alignment (the device copies keep it mod 16)."""
+    """Both entry points copy results back slot by slot (touching slots merged):
+    the bytes of `out` / `text` before the first slot, between slots and after
+    the last stay as they were, whatever the slots' alignment (the device
+    copies keep it mod 16)."""
     rng = np.random.default_rng(3)
     datas = [rng.integers(0, 256, n, dtype=np.uint8).tobytes() for n in (1000, 77, 4099)]
     exp = np.frombuffer(b"".join(hashlib.sha1(d).digest() for d in datas), dtype=np.uint8).reshape(-1, 20)
@@ -251,3 +252,125 @@ def test_outputs_touch_nothing_outside_their_slots(hasher):
         assert (tbuf[:first] == 0xCD).all() and (tbuf[int(tslot[-1]) + lens[2]:] == 0xCD).all()
         for i, t in enumerate(texts):
             assert tbuf[int(tslot[i]):int(tslot[i]) + len(t)].tobytes() == t
+
+
+def _encoder_layout_sizes():
+    """Chunk sizes whose text exercises every length form of the encoder's
+    layout and the one-pass kernels' tiles (64 lines = 3,456 bytes = 4,672
+    characters): no tail, one or two tail bytes, a padded last group that is
+    the 18th of its line (length 73q + 72: 52, 53, 106, 107, ...), a text that
+    ends with a separator (54k bytes), tile edges, a C5 chunk."""
+    s = {0, 1, 2, 3, 51, 52, 53, 54, 55, 105, 106, 107, 108, 161, 162}
+    for k in (1, 2, 3, 76):
+        for d in (-3, -2, -1, 0, 1, 2, 3):
+            s.add(3456 * k + d)
+    for g in (17, 35, 18 * 64 - 1, 18 * 64 + 17, 18 * 200 + 17):  # full groups = 18q + 17
+        s.update({3 * g + 1, 3 * g + 2})
+    s.update({65536, 262144, 262145, 262146})
+    return sorted(s)
+
+
+@pytest.mark.parametrize("align,shift", [(16, 0), (16, 5), (4, 2)])
+def test_one_pass_takes_every_encoder_layout(hasher, align, shift):
+    """Every text the encoder writes takes the one-pass kernel (the general
+    decode sees none of them), including a padded last group that is the 18th
+    of its line (such lengths, 73q + 72, went to the general
+    kernel before), at aligned and unaligned text and output slots; bytes,
+    lengths and verdicts equal the reference decoder's.  Damaged texts of the
+    same lengths go to the general kernel."""
+    rng = np.random.default_rng(40 + shift)
+    sizes = _encoder_layout_sizes()
+    datas = [rng.integers(0, 256, n, dtype=np.uint8).tobytes() for n in sizes]
+    texts = [xmlrpc_text(d) for d in datas]
+    for d, t in zip(datas, texts):
+        if len(t) % 73 == 72:
+            assert t[-1:] == b"=", len(d)  # the form ADVICE r04 named: a padded group ends the line
+    s0 = hasher.b64_stats()
+    ver, dec, out, ooff, esz = _batch(hasher, texts, datas, align, shift)
+    s1 = hasher.b64_stats()
+    assert ver.all(), [sizes[i] for i in np.nonzero(~ver)[0]]
+    assert list(dec) == sizes
+    for i, d in enumerate(datas):
+        assert out[int(ooff[i]):int(ooff[i]) + len(d)].tobytes() == d, sizes[i]
+    assert s1["one_pass"] - s0["one_pass"] == len(sizes) and s1["general"] == s0["general"]
+    # one alphabet character of each non-empty text replaced by junk: same lengths, general path, verdict 0
+    bad = [bytearray(t) for t in texts]
+    for t in bad:
+        if t:
+            alpha = [j for j, c in enumerate(t) if _DEC[c] < 64]
+            t[alpha[int(rng.integers(0, len(alpha)))]] = ord("*")
+    ver, dec, *_ = _batch(hasher, [bytes(t) for t in bad], datas, align, shift)
+    s2 = hasher.b64_stats()
+    nonempty = sum(1 for t in texts if t)
+    assert s2["general"] - s1["general"] == nonempty
+    for i, t in enumerate(bad):
+        w = b64get(bytes(t))
+        assert int(dec[i]) == (len(w) if len(w) <= sizes[i] else sizes[i] + 1), sizes[i]
+        assert bool(ver[i]) == (w == datas[i]), sizes[i]
+
+
+@pytest.mark.parametrize("one_pass", [True, False])
+def test_gaps_between_slots_are_never_written(hasher, one_pass):
+    """the decoded bytes come back slot by slot, so bytes of
+    `out` between slots keep the caller's data (a shared or file-mapped arena),
+    and a slot's bytes past a short decode are zeros, never another batch's
+    device bytes.  Same for the encoder's text slots."""
+    rng = np.random.default_rng(9)
+    sizes = [5000, 3456, 77, 262144, 1]
+    datas = [rng.integers(0, 256, n, dtype=np.uint8).tobytes() for n in sizes]
+    texts = [xmlrpc_text(d) for d in datas]
+    texts[2] = xmlrpc_text(datas[2][:40])  # short: decodes to 40 of 77 bytes
+    if not one_pass:
+        texts = [b"\x01" + t for t in texts]  # junk in front: the general kernel decodes them all
+    # a previous call leaves other bytes in the device scratch
+    _batch(hasher, [xmlrpc_text(bytes([0xEE]) * 300000)], [bytes([0xEE]) * 300000])
+    gaps = [7, 0, 100, 13, 3]  # bytes before each slot
+    ooff, pos = [], 0
+    for g, n in zip(gaps, sizes):
+        pos += g
+        ooff.append(pos)
+        pos += n
+    out = np.full(pos + 9, 0x5A, dtype=np.uint8)
+    toffs, buf = [], bytearray()
+    for t in texts:
+        toffs.append(len(buf))
+        buf += t
+    exp = np.frombuffer(b"".join(hashlib.sha1(d).digest() for d in datas), dtype=np.uint8).reshape(-1, 20)
+    ver, dec = hasher.verify_b64(np.frombuffer(bytes(buf), np.uint8), toffs, [len(t) for t in texts], sizes, exp,
+                                 out, np.array(ooff, dtype=np.uint64))
+    assert list(ver) == [True, True, False, True, True]
+    assert list(dec) == [5000, 3456, 40, 262144, 1]
+    inside = np.zeros(out.size, dtype=bool)
+    for o, n in zip(ooff, sizes):
+        inside[o:o + n] = True
+    assert (out[~inside] == 0x5A).all(), "a byte outside the slots was written"
+    for i, (o, d) in enumerate(zip(ooff, datas)):
+        got = out[o:o + sizes[i]].tobytes()
+        assert got == (d if i != 2 else d[:40] + bytes(37)), i
+
+
+def test_overlapping_slots_are_refused(hasher):
+    """ADVICE r04: two chunks' results in one byte would race on the device;
+    both entry points refuse overlapping output slots."""
+    from bitflood_amd import LbfError
+    d = bytes(range(200))
+    t = xmlrpc_text(d)
+    text = np.frombuffer(t + t, np.uint8)
+    exp = np.frombuffer(hashlib.sha1(d).digest() * 2, np.uint8).reshape(2, 20)
+    out = np.zeros(600, np.uint8)
+    with pytest.raises(LbfError, match="overlaps"):
+        hasher.verify_b64(text, [0, len(t)], [len(t)] * 2, [200, 200], exp, out, np.array([0, 199], np.uint64))
+    ver, _ = hasher.verify_b64(text, [0, len(t)], [len(t)] * 2, [200, 200], exp, out, np.array([0, 200], np.uint64))
+    assert ver.all()  # touching slots are fine
+    data = np.frombuffer(d, np.uint8)
+    offs = np.zeros(2, np.uint64)
+    sz = np.array([200, 200], np.uint32)
+    v = np.zeros(2, np.uint8)
+    tbuf = np.zeros(1000, np.uint8)
+    e = np.ascontiguousarray(exp)
+    for tslot, rc_ok in (([0, len(t) - 1], False), ([0, len(t)], True)):
+        ts = np.array(tslot, np.uint64)
+        rc = hasher._lib.lbf_verify_encode_b64_batch(hasher._h, data.ctypes.data, data.size, offs.ctypes.data,
+                                                     sz.ctypes.data, 2, e.ctypes.data, v.ctypes.data,
+                                                     tbuf.ctypes.data, tbuf.size, ts.ctypes.data)
+        assert (rc == 0) is rc_ok, rc

@@ -217,3 +217,29 @@ def test_memory_pinned_elsewhere_is_used_only_when_one_allocation_holds_it(oracl
     finally:
         assert hip.hipHostUnregister(ctypes.c_void_p(base)) == 0
         assert hip.hipHostUnregister(ctypes.c_void_p(base + 2 * MIB)) == 0
+
+
+@pytest.mark.parametrize("size", [3 * MIB, 3 * MIB + 12345])
+def test_buffer_the_caller_pinned_whole_goes_direct(oracle, hasher, size):
+    """a buffer the caller pinned whole with hipHostRegister (its own
+    registration, possibly not ending on a page) is registered as it is and
+    read straight from the caller's memory, never unpinned by the library."""
+    import ctypes
+    import mmap
+    hip = _hip()
+    mm = mmap.mmap(-1, 4 * MIB)
+    buf = np.frombuffer(mm, dtype=np.uint8)[:size]
+    base = buf.ctypes.data
+    assert hip.hipHostRegister(ctypes.c_void_p(base), size, 0) == 0
+    try:
+        buf[:] = oracle.synth(93, 0, size, nthreads=4)
+        offs, sizes = chunk_table(buf.size, 256 * 1024)
+        want = oracle.sha1_batch(buf, offs, sizes, nthreads=4)
+        hasher.register_host(buf)
+        s0 = hasher.staging_stats()
+        assert np.array_equal(hasher.hash_chunks(buf, offs, sizes), want)
+        assert _delta(hasher, s0)["direct"] == buf.size
+        hasher.unregister_host(buf)
+        assert np.array_equal(hasher.hash_chunks(buf, offs, sizes), want)
+    finally:
+        assert hip.hipHostUnregister(ctypes.c_void_p(base)) == 0
