@@ -890,6 +890,142 @@ constexpr uint64_t kJoinGap = 4096;
 // knob) caps the job size that goes direct; by default every size does.
 constexpr uint64_t kDirectMinRun = 1ull << 20;
 
+// Pinning a large pageable job on the fly (LBF_AUTOPIN=1, an A/B knob, off by
+// default).  A pageable job crosses host DRAM three times on
+// the staged route (the caller's write, the staging memcpy's read and write,
+// the DMA's read) and its rate moves with the box's memcpy; a registered one
+// crosses it once (§3).  Here a helper thread pins the job's address span in
+// windows of LBF_AUTOPIN_MB (256 MiB) ahead of the worker, at most
+// kAhead windows past the one being copied; a group whose bytes lie in pinned
+// windows goes the direct route, and each window is unpinned once the worker
+// has moved past it and its last copy has landed (an event recorded after that
+// copy).  A window HIP refuses to pin (pinned elsewhere) stays on the staged route.
+class AutoPin {
+ public:
+  AutoPin(int device, uintptr_t lo, uintptr_t hi, uint64_t window) : device_(device) {
+    const uintptr_t page = (uintptr_t)sysconf(_SC_PAGESIZE);
+    lo &= ~(page - 1);
+    hi = (hi + page - 1) & ~(page - 1);
+    window = std::max<uint64_t>(page, window / page * page);
+    for (uintptr_t a = lo; a < hi; a += window) win_.push_back(Window{a, std::min<uintptr_t>(hi, a + window)});
+    for (Window& w : win_)
+      if (hipEventCreateWithFlags(&w.ev, hipEventDisableTiming) != hipSuccess) {
+        (void)hipGetLastError();
+        w.ev = nullptr;
+      }
+    th_ = std::thread([this] { loop(); });
+  }
+  ~AutoPin() { finish(); }
+  // true once every window holding [a, b) is pinned; waits for the helper to get there
+  bool covered(uintptr_t a, uintptr_t b) {
+    std::unique_lock<std::mutex> g(mu_);
+    const size_t k0 = index(a), k1 = index(b - 1);
+    if (k0 >= win_.size() || k1 >= win_.size()) return false;
+    cursor_ = std::max(cursor_, k1);  // the helper pins up to kAhead windows past this group
+    cv_.notify_all();
+    for (size_t k = k0; k <= k1; ++k) {
+      cv_.wait(g, [&] { return win_[k].state != kPending || stop_; });
+      if (win_[k].state != kPinned) return false;
+    }
+    return true;
+  }
+  // a group's copies from [a, b) were issued on `stream`: record each window's
+  // event behind them (the last recording is the one its unpin waits for)
+  bool used(uintptr_t a, uintptr_t b, hipStream_t stream) {
+    std::lock_guard<std::mutex> g(mu_);
+    for (size_t k = index(a); k <= index(b - 1) && k < win_.size(); ++k) {
+      if (!win_[k].ev || hipEventRecord(win_[k].ev, stream) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+      }
+      win_[k].used = true;
+    }
+    return true;
+  }
+  // the worker will not read below `a` again: windows that end there can go
+  void retire_before(uintptr_t a) {
+    std::lock_guard<std::mutex> g(mu_);
+    while (retired_ < win_.size() && win_[retired_].hi <= a) ++retired_;
+    cv_.notify_all();
+  }
+  // every stream drained: unpin whatever is left and stop the helper
+  void finish() {
+    if (!th_.joinable()) return;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      retired_ = win_.size();
+      stop_ = true;
+    }
+    cv_.notify_all();
+    th_.join();
+    for (Window& w : win_)
+      if (w.ev) (void)hipEventDestroy(w.ev);
+  }
+  uint64_t pinned_bytes() const { return pinned_bytes_; }
+
+ private:
+  static constexpr int kPending = 0, kPinned = 1, kFailed = 2, kUnpinned = 3;
+  static constexpr size_t kAhead = 4;
+  struct Window {
+    uintptr_t lo, hi;
+    int state = kPending;
+    hipEvent_t ev = nullptr;
+    bool used = false;
+  };
+  size_t index(uintptr_t a) const {
+    if (win_.empty() || a < win_[0].lo) return win_.size();
+    const uint64_t w = win_[0].hi - win_[0].lo;
+    return (size_t)((a - win_[0].lo) / w);
+  }
+  void loop() {
+    (void)hipSetDevice(device_);
+    size_t next = 0, unpinned = 0;  // windows pinned (or refused) so far; windows unpinned so far
+    std::unique_lock<std::mutex> g(mu_);
+    for (;;) {
+      // retired windows first: the worker does not read their pages again
+      while (unpinned < std::min(retired_, next)) {
+        Window& w = win_[unpinned++];
+        if (w.state != kPinned) continue;
+        g.unlock();
+        if (w.used && w.ev) (void)hipEventSynchronize(w.ev);  // its last copy has landed
+        (void)hipHostUnregister(reinterpret_cast<void*>(w.lo));
+        (void)hipGetLastError();
+        g.lock();
+        w.state = kUnpinned;
+      }
+      if (stop_) {  // finish(): every window retired; none is pinned past this point
+        for (size_t k = next; k < win_.size(); ++k) win_[k].state = kFailed;
+        cv_.notify_all();
+        if (unpinned >= next) return;
+        continue;
+      }
+      if (next < win_.size() && next <= cursor_ + kAhead) {
+        Window& w = win_[next];
+        g.unlock();
+        const hipError_t e = hipHostRegister(reinterpret_cast<void*>(w.lo), w.hi - w.lo, hipHostRegisterPortable);
+        if (e != hipSuccess) (void)hipGetLastError();  // pinned elsewhere, or no memory: that window is staged
+        g.lock();
+        w.state = e == hipSuccess ? kPinned : kFailed;
+        if (e == hipSuccess) pinned_bytes_ += w.hi - w.lo;
+        ++next;
+        cv_.notify_all();
+        continue;
+      }
+      cv_.wait(g, [&] {
+        return stop_ || unpinned < std::min(retired_, next) || (next < win_.size() && next <= cursor_ + kAhead);
+      });
+    }
+  }
+  int device_;
+  std::vector<Window> win_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  size_t cursor_ = 0, retired_ = 0;
+  bool stop_ = false;
+  uint64_t pinned_bytes_ = 0;
+  std::thread th_;
+};
+
 // Process descriptors [begin, end) on one worker.  They are staged in source
 // order: sorted by offset (a stable permutation, skipped when the table is
 // already sorted, as every file-order table is).  A group is a run of
@@ -923,6 +1059,7 @@ int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
       break;
     }
   uint64_t job_bytes = 0;  // the union of this worker's runs
+  uint64_t span_lo = UINT64_MAX, span_hi = 0;  // the address span they lie in (memory jobs)
   {
     // Staging sized to the bytes this worker stages (the union of its runs):
     // a quarter of them per slot once they exceed kSplitMin, so a mid-sized job
@@ -936,6 +1073,8 @@ int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
       const uint64_t k = order(q), o = job.offsets[k], sz = job.sizes[k];
       if (sz == 0 || sz + 15 > w.slot_max) continue;
       largest = std::max(largest, sz);
+      span_lo = std::min(span_lo, o);
+      span_hi = std::max(span_hi, o + sz);
       if (open && job.file(k) == run_file && o <= run_end + kJoinGap) {
         if (o + sz > run_end) bytes += o + sz - run_end, run_end = o + sz;
       } else {
@@ -967,6 +1106,18 @@ int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
   const uint64_t direct_max_mb = env_u64("LBF_DIRECT_MAX_MB", 0);
   const uint64_t direct_max = direct_max_mb ? direct_max_mb << 20 : UINT64_MAX;
   const bool direct_job = job.src.pinned && job_bytes <= direct_max;
+  // LBF_AUTOPIN=1 (A/B knob): pin a large pageable job on the fly (AutoPin above);
+  // only when its runs fill at least half of their address span
+  std::unique_ptr<AutoPin> autopin;
+  if (!job.src.pinned && !job.src.from_files() && env_long("LBF_AUTOPIN", 0) == 1 && span_hi > span_lo &&
+      job_bytes >= (env_u64("LBF_AUTOPIN_MIN_MB", 256) << 20) && 2 * job_bytes >= span_hi - span_lo) {
+    const uintptr_t b = reinterpret_cast<uintptr_t>(job.src.base);
+    try {
+      autopin.reset(new AutoPin(w.device, b + span_lo, b + span_hi, env_u64("LBF_AUTOPIN_MB", 256) << 20));
+    } catch (const std::exception&) {
+      autopin.reset();  // no helper thread: the staged route, as without the knob
+    }
+  }
   int cur = 0, hcur = 0;
   int prev_direct = -1;  // device slot of the last direct-route batch
   uint64_t i = begin;
@@ -1037,7 +1188,14 @@ int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
       // part comes back short (EOF), the rest of that run is unavailable.
       // A registered source skips the ring: each run is copied to the device
       // straight from the caller's pinned memory, then the header follows.
-      const bool direct = direct_job && !runs.empty() && cursor >= runs.size() * kDirectMinRun;
+      bool direct = direct_job && !runs.empty() && cursor >= runs.size() * kDirectMinRun;
+      const uintptr_t g_lo = runs.empty() ? 0 : reinterpret_cast<uintptr_t>(job.src.base) + runs.front().src;
+      const uintptr_t g_hi = runs.empty() ? 0 : reinterpret_cast<uintptr_t>(job.src.base) + runs.back().src +
+                                                     runs.back().len;
+      if (autopin && !runs.empty()) {
+        autopin->retire_before(g_lo);  // runs come in address order: nothing below this group is read again
+        direct = cursor >= runs.size() * kDirectMinRun && autopin->covered(g_lo, g_hi);
+      }
       const bool single = !direct && hdr + cursor <= w.pin_bytes;
       const uint64_t data_off = single ? hdr : w.hdr_cap;
       uint8_t* h_header = nullptr;
@@ -1068,6 +1226,10 @@ int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
           r.avail = r.len;
         }
         if (rc || !hip_ok(hipEventRecord(s.copied, s.stream), "hipEventRecord")) break;
+        if (autopin && !autopin->used(g_lo, g_hi, s.stream)) {
+          rc = fail(LBF_ERR_HIP, "hipEventRecord (on-the-fly pinning)");
+          break;
+        }
         prev_direct = cur;
       }
       (direct ? w.bytes_direct : w.bytes_staged) += cursor;
@@ -1168,6 +1330,7 @@ int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
     s.pending = false;
   }
   for (HostSlot& h : w.host) h.in_flight = false;
+  if (autopin) autopin->finish();  // every copy has landed (drained above): unpin the rest
   trim_dev_slots(w);
   return rc;
 }

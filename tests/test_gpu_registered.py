@@ -243,3 +243,37 @@ def test_buffer_the_caller_pinned_whole_goes_direct(oracle, hasher, size):
         assert np.array_equal(hasher.hash_chunks(buf, offs, sizes), want)
     finally:
         assert hip.hipHostUnregister(ctypes.c_void_p(base)) == 0
+
+
+@pytest.mark.parametrize("mib,piece_pinned", [(600, False), (600, True)])
+def test_on_the_fly_pinning_knob(oracle, hasher, monkeypatch, mib, piece_pinned):
+    """LBF_AUTOPIN=1 (the A/B knob of DESIGN.md §9.6): a large pageable job is
+    pinned window by window while it copies, goes the direct route, and leaves
+    nothing pinned behind; a window HIP refuses (pinned elsewhere) is staged.
+    Digests equal the oracle's either way."""
+    import ctypes
+    hip = _hip()
+    monkeypatch.setenv("LBF_AUTOPIN", "1")
+    monkeypatch.setenv("LBF_AUTOPIN_MB", "64")
+    buf = oracle.synth(95, 0, mib * MIB + 4321, nthreads=8)
+    offs, sizes = chunk_table(buf.size, 256 * 1024)
+    want = oracle.sha1_batch(buf, offs, sizes, nthreads=8)
+    page = 4096
+    other = None
+    if piece_pinned:  # someone else holds 8 MiB in the middle
+        other = (buf.ctypes.data + 300 * MIB) // page * page
+        assert hip.hipHostRegister(ctypes.c_void_p(other), 8 * MIB, 0) == 0
+    try:
+        s0 = hasher.staging_stats()
+        assert np.array_equal(hasher.hash_chunks(buf, offs, sizes), want)
+        d = _delta(hasher, s0)
+        assert d["direct"] > buf.size // 2 and d["direct"] + d["staged"] >= buf.size
+        if piece_pinned:
+            assert d["staged"] > 0
+    finally:
+        if other:
+            assert hip.hipHostUnregister(ctypes.c_void_p(other)) == 0
+    # nothing of the job is left pinned: the caller can pin it all itself
+    base = buf.ctypes.data // page * page
+    assert hip.hipHostRegister(ctypes.c_void_p(base), buf.ctypes.data + buf.size - base, 0) == 0
+    assert hip.hipHostUnregister(ctypes.c_void_p(base)) == 0

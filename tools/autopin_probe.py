@@ -10,6 +10,9 @@ all in one process and lease, best of 3 after a warm pass:
   reg_pipelined pieces of --piece-mib: a helper thread registers piece k+1 (and
                 unregisters piece k-1) while piece k is hashed straight from
                 pinned memory; registration and hashing timed together
+  autopin       the library's own on-the-fly pinning (LBF_AUTOPIN=1: a helper
+                thread pins windows of LBF_AUTOPIN_MB ahead of the copies and
+                unpins them behind; lbf_capi.cpp AutoPin)
   registered    the buffer registered outside the timing (what a caller that
                 reuses its buffer gets: the ceiling of the pinned routes)
 plus the cost of pinning and unpinning alone (GiB/s of hipHostRegister /
@@ -98,6 +101,15 @@ def main():
                 assert bytes(last[-1]) == want_last
             r["reg_pipelined"] = best_of(3, pipelined)
 
+            os.environ["LBF_AUTOPIN"] = "1"
+            s0 = h.staging_stats()
+            g = h.hash_chunks(data, offs, sizes_)
+            assert bytes(g[-1]) == want_last
+            r["autopin"] = best_of(3, lambda: h.hash_chunks(data, offs, sizes_))
+            autopin_direct = (h.staging_stats()["direct"] - s0["direct"]) / (4 * data.size)
+            os.environ["LBF_AUTOPIN"] = "0"
+            r["staged_again"] = best_of(3, lambda: h.hash_chunks(data, offs, sizes_))
+
             t = time.perf_counter()
             h.register_host(data)
             reg_s = time.perf_counter() - t
@@ -111,7 +123,8 @@ def main():
             out["pin"][mib] = {"register_s": round(reg_s, 4), "unregister_s": round(unreg_s, 4),
                                "register_gibs": round(data.size / reg_s / 2**30, 1),
                                "unregister_gibs": round(data.size / unreg_s / 2**30, 1),
-                               "registered_direct_fraction": round(direct / (3 * data.size), 3)}
+                               "registered_direct_fraction": round(direct / (3 * data.size), 3),
+                               "autopin_direct_fraction": round(autopin_direct, 3)}
             print(json.dumps({mib: out["gibs"][mib], "pin": out["pin"][mib]}), file=sys.stderr, flush=True)
     print(json.dumps(out), flush=True)
 
