@@ -117,7 +117,14 @@ def load() -> ctypes.CDLL:
                        f"{LIB_PATH} is not built; run `python -c 'import __graft_entry__ as g; g.build()'`")
     lib = ctypes.CDLL(LIB_PATH)
     for name, (res, args) in _SIGS.items():
-        fn = getattr(lib, name)
+        try:
+            fn = getattr(lib, name)
+        except AttributeError:
+            # an A/B build of an earlier round (LBF_LIB, tools only) may lack
+            # entry points added since; the shipped library must have them all
+            if "LBF_LIB" in os.environ:
+                continue
+            raise
         fn.restype = res
         fn.argtypes = args
     _lib = lib

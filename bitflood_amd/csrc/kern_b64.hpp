@@ -111,22 +111,34 @@ typedef uint32_t b64_u32x4 __attribute__((ext_vector_type(4)));  // what the non
 // hold them: afterwards lds byte (delta + k) = src[k], delta = src mod 16.  The
 // blocks are read whole (a 16-byte block holding one byte of the span lies in
 // the same page, so this never reads an unmapped address).  Up to two blocks
-// per lane, both loads issued before either store.
-template <uint32_t kBlocks>
-__device__ __forceinline__ uint32_t b64_stage_span(const uint8_t* src, uint32_t len, uint4* lds) {
-  static_assert(kBlocks <= 2 * kB64Threads, "two blocks per lane at most");
-  const uintptr_t a = reinterpret_cast<uintptr_t>(src);
-  const uint32_t delta = (uint32_t)(a & 15u);
-  const b64_u32x4* g = reinterpret_cast<const b64_u32x4*>(a - delta);
-  b64_u32x4* l = reinterpret_cast<b64_u32x4*>(lds);
-  const uint32_t blocks = (delta + len + 15) / 16;
-  const uint32_t k0 = threadIdx.x, k1 = threadIdx.x + kB64Threads;
+// per lane.  load() issues both of a lane's loads and returns at once; store()
+// waits for them and writes LDS, so work placed between the two (the decode
+// table, the last group's check) runs while the loads are in flight.
+struct B64Stage {
   b64_u32x4 v0, v1;
-  if (k0 < blocks) v0 = __builtin_nontemporal_load(g + k0);
-  if (k1 < blocks) v1 = __builtin_nontemporal_load(g + k1);
-  if (k0 < blocks) l[k0] = v0;
-  if (k1 < blocks) l[k1] = v1;
-  return delta;
+  uint32_t blocks = 0, delta = 0;
+  __device__ __forceinline__ void load(const uint8_t* src, uint32_t len) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(src);
+    delta = (uint32_t)(a & 15u);
+    const b64_u32x4* g = reinterpret_cast<const b64_u32x4*>(a - delta);
+    blocks = (delta + len + 15) / 16;
+    const uint32_t k0 = threadIdx.x, k1 = threadIdx.x + kB64Threads;
+    if (k0 < blocks) v0 = __builtin_nontemporal_load(g + k0);
+    if (k1 < blocks) v1 = __builtin_nontemporal_load(g + k1);
+  }
+  __device__ __forceinline__ void store(uint4* lds) const {
+    b64_u32x4* l = reinterpret_cast<b64_u32x4*>(lds);
+    const uint32_t k0 = threadIdx.x, k1 = threadIdx.x + kB64Threads;
+    if (k0 < blocks) l[k0] = v0;
+    if (k1 < blocks) l[k1] = v1;
+  }
+};
+
+// The decode table entry of character c (B64Table), computed: filling the LDS
+// copy this way costs a few VALU per lane and no dependent global load.
+__device__ __forceinline__ uint32_t b64_value(uint32_t c) {
+  return c - 'A' < 26u ? c - 'A' : c - 'a' < 26u ? c - 'a' + 26 : c - '0' < 10u ? c - '0' + 52 :
+         c == '+' ? 62u : c == '/' ? 63u : c == '=' ? (uint32_t)kB64Eq : (uint32_t)kB64Skip;
 }
 
 // Four bytes of LDS from any byte address (two aligned dword reads + v_alignbyte).
@@ -174,7 +186,7 @@ __device__ __forceinline__ bool b64_canon_groups(uint32_t len, uint32_t* groups)
   return true;
 }
 
-// blockIdx.x = (chunk - chunk0) * tiles + tile.  Chunk i's text is
+// blockIdx.x = tile, blockIdx.y = chunk - chunk0.  Chunk i's text is
 // text[text_off[i] .. + text_len[i]); its decoded bytes go to
 // out[out_off[i] .. + cap[i]): bytes [0, min(decoded, cap)) decoded, the rest
 // of the slot zeroed, so a short text never leaves stale device bytes in the
@@ -189,10 +201,13 @@ __global__ void __launch_bounds__(kB64Threads) b64_decode_canon_kernel(const uin
                                                                        uint8_t* __restrict__ over,
                                                                        uint8_t* __restrict__ redo, uint32_t tiles,
                                                                        uint32_t chunk0) {
-  constexpr uint32_t kStage = (kB64TileText + 15 + 15) / 16 + 1;  // the span, its phase, one block of slack
+  // the span, its phase, and slack for the last lane's 32-byte window read
+  constexpr uint32_t kStage = (kB64TileText + 15 + 15) / 16 + 2;
+  static_assert(kStage <= 2 * kB64Threads, "two blocks per lane at most");
   __shared__ uint4 stage[kStage];
   __shared__ uint8_t tab[256];
-  const uint32_t i = chunk0 + blockIdx.x / tiles, tile = blockIdx.x % tiles;
+  __shared__ uint32_t last_shared;
+  const uint32_t i = chunk0 + blockIdx.y, tile = blockIdx.x;
   const uint32_t len = text_len[i];
   uint32_t groups = 0;
   if (!b64_canon_groups(len, &groups)) {  // the whole workgroup leaves: no barrier below is reached
@@ -201,46 +216,74 @@ __global__ void __launch_bounds__(kB64Threads) b64_decode_canon_kernel(const uin
   }
   const uint32_t limit = cap[i];
   const uint32_t tbeg = tile * kB64TileText, obeg = tile * kB64TileBytes;
+  if (tbeg >= len && obeg >= limit && tile != 0) return;  // past this chunk's text and slot (the whole workgroup)
   const uint8_t* t = text + text_off[i];
-  // the last group: "xxxx", "xxx=" or "xx==" sets the decoded length
-  uint32_t last = 3;
-  bool bad = false;
-  if (groups > 0) {
-    const uint32_t g = groups - 1, at = 4 * g + g / 18;
-    const uint8_t c2 = g_b64_table.v[t[at + 2]], c3 = g_b64_table.v[t[at + 3]];
-    last = c3 < 64 ? 3u : c2 < 64 ? 2u : 1u;
-    bad = c3 == kB64Skip || c2 == kB64Skip || (c2 == kB64Eq && c3 != kB64Eq);
+  B64Stage st;
+  if (tbeg < len) st.load(t + tbeg, min(kB64TileText, len - tbeg));
+  tab[threadIdx.x] = (uint8_t)b64_value(threadIdx.x);
+  if (threadIdx.x == 0) {
+    // the last group -- "xxxx", "xxx=" or "xx==" -- sets the decoded length
+    uint32_t last = 3;
+    bool bad = false;
+    if (groups > 0) {
+      const uint32_t g = groups - 1, at = 4 * g + g / 18;
+      const uint32_t c2 = b64_value(t[at + 2]), c3 = b64_value(t[at + 3]);
+      last = c3 < 64 ? 3u : c2 < 64 ? 2u : 1u;
+      bad = c3 == kB64Skip || c2 == kB64Skip || (c2 == kB64Eq && c3 != kB64Eq);
+    }
+    last_shared = last;
+    if (tile == 0) {
+      const uint64_t want = groups ? 3ull * (groups - 1) + last : 0;
+      sizes[i] = (uint32_t)min<uint64_t>(want, limit);
+      over[i] = want > limit ? 1 : 0;
+      if (bad) redo[i] = 1;
+    }
   }
-  const uint64_t want = groups ? 3ull * (groups - 1) + last : 0;
-  if (tile == 0 && threadIdx.x == 0) {
-    sizes[i] = (uint32_t)min<uint64_t>(want, limit);
-    over[i] = want > limit ? 1 : 0;
-    if (bad) redo[i] = 1;
-  }
-  if (tbeg >= len && obeg >= limit) return;  // a tile past this chunk's text and slot (the whole workgroup)
-  tab[threadIdx.x] = g_b64_table.v[threadIdx.x];
-  const uint32_t delta = tbeg < len ? b64_stage_span<kStage>(t + tbeg, min(kB64TileText, len - tbeg), stage) : 0u;
+  st.store(stage);
+  const uint32_t delta = st.delta;
   __syncthreads();
+  const uint64_t want = groups ? 3ull * (groups - 1) + last_shared : 0;
+  if (tbeg >= len && obeg >= limit) return;  // tile 0 of an empty chunk with an empty slot
   const uint32_t* w = reinterpret_cast<const uint32_t*>(stage);
   const uint8_t* sb = reinterpret_cast<const uint8_t*>(stage);
+  bool bad = false;
   if (threadIdx.x < kB64TileBytes / 16) {
-    // bytes [16u, 16u + 16) of the tile come from its groups g0 .. g0 + 5
+    // Bytes [16u, 16u + 16) of the tile come from its groups g0 .. g0 + 5, whose
+    // characters lie in [c0, c0 + 25): 24 characters and at most one
+    // separator, after group 17 - r0 of the window when r0 >= 12.  One window
+    // of eight aligned dwords holds them; each group's four characters are cut
+    // out of it with v_alignbyte (no divergent branch: groups past the chunk's
+    // end are decoded from whatever lies there and masked below).
     const uint32_t b0 = 16 * threadIdx.x, g0 = b0 / 3, phase = b0 - 3 * g0;
+    const uint32_t l0 = g0 / 18, r0 = g0 - 18 * l0;
+    const uint32_t c0 = delta + 4 * g0 + l0, sh0 = c0 & 3u;
+    const uint32_t* wb = w + (c0 >> 2);
+    uint32_t win[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) win[k] = wb[k];
+    const uint32_t gbase = tile * kB64TileGroups + g0;  // the chunk's index of group g0
     uint32_t x[6];
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
-      const uint32_t gl = g0 + j, gg = tile * kB64TileGroups + gl;
-      x[j] = 0;
-      if (gg < groups) {
-        const uint32_t at = delta + 4 * gl + gl / 18;
-        const uint32_t c = lds_u32_at(w, at);
-        const uint32_t s0 = tab[c & 255], s1 = tab[(c >> 8) & 255], s2 = tab[(c >> 16) & 255], s3 = tab[c >> 24];
-        // inside the text every character is in the alphabet; the last
-        // group's padding was checked above
-        bad |= gg + 1 < groups ? (s0 | s1 | s2 | s3) >= 64 : (s0 | s1) >= 64;
-        if (gl % 18 == 17 && 4 * gg + gg / 18 + 4 < len) bad |= tab[sb[at + 4]] != kB64Skip;  // the separator
-        x[j] = ((s0 & 63) << 18) | ((s1 & 63) << 12) | ((s2 & 63) << 6) | (s3 & 63);
-      }
+      const uint32_t sep = r0 + j >= 18 ? 1u : 0u;
+      const uint32_t o = sh0 + sep;  // 0..4: this group's offset from dword j of the window
+      const uint32_t lo = o >= 4 ? win[j + 1] : win[j], hi = o >= 4 ? win[j + 2] : win[j + 1];
+      const uint32_t c = __builtin_amdgcn_alignbyte(hi, lo, o & 3u);
+      const uint32_t s0 = tab[c & 255], s1 = tab[(c >> 8) & 255], s2 = tab[(c >> 16) & 255], s3 = tab[c >> 24];
+      const uint32_t gg = gbase + j;
+      // inside the text every character is in the alphabet; the last group's
+      // padding was checked above
+      const bool inner = ((s0 | s1 | s2 | s3) & ~63u) != 0, head = ((s0 | s1) & ~63u) != 0;
+      bad |= (gg + 1 < groups && inner) || (gg + 1 == groups && head);
+      x[j] = ((s0 & 63) << 18) | ((s1 & 63) << 12) | ((s2 & 63) << 6) | (s3 & 63);
+    }
+    // the separator after group 17 - r0 (when in the window): any character outside the alphabet
+    {
+      const uint32_t js = 17 - r0;  // < 6 when r0 >= 12
+      const uint32_t gs = gbase + js;
+      const uint32_t at = (c0 & ~3u) + min(sh0 + 4 * js + 4, 31u);
+      const bool check = r0 >= 12 && 4 * gs + gs / 18 + 4 < len;
+      bad |= check && tab[sb[at]] != kB64Skip;
     }
     // the 18 bytes of the six groups, as little-endian words
     auto by = [&](int j, int k) { return (x[j] >> (16 - 8 * k)) & 255u; };
@@ -418,7 +461,7 @@ __host__ __device__ constexpr uint64_t b64_put_length(uint64_t size) {
   return 4 * (size / 3) + (size % 3 ? 4 : 0) + size / 3 / 18;
 }
 
-// blockIdx.x = (chunk - chunk0) * tiles + tile: tile k of chunk i encodes bytes
+// blockIdx.x = tile, blockIdx.y = chunk - chunk0: tile k of chunk i encodes bytes
 // [3456k, +3456) into text [4672k, +4672) (clipped to the chunk).  Each lane
 // writes one 16-byte block of the text: characters [p, p + 16) of a line lie
 // in at most five consecutive "words" of the line's character stream, where
@@ -434,19 +477,22 @@ __global__ void __launch_bounds__(kB64Threads) b64_encode_kernel(const uint8_t* 
   // the span, its phase, and slack for the group reads of the last window
   // (computed for every word, used only inside the tile)
   constexpr uint32_t kStage = (kB64TileBytes + 15) / 16 + 4;
+  static_assert(kStage <= 2 * kB64Threads, "two blocks per lane at most");
   __shared__ uint4 stage[kStage];
   __shared__ uint8_t alpha[64];
-  const uint32_t i = chunk0 + blockIdx.x / tiles, tile = blockIdx.x % tiles;
+  const uint32_t i = chunk0 + blockIdx.y, tile = blockIdx.x;
   const uint32_t n = size[i], full = n / 3, rest = n % 3;
   const uint64_t tl = b64_put_length(n);
   const uint32_t tbeg = tile * kB64TileText, dbeg = tile * kB64TileBytes;
   if (tbeg >= tl) return;  // the whole workgroup: no barrier below is reached
+  B64Stage st;
+  if (dbeg < n) st.load(data + data_off[i] + dbeg, min(kB64TileBytes, n - dbeg));
   if (threadIdx.x < 64) {
     const uint32_t c = threadIdx.x;
     alpha[c] = (uint8_t)(c < 26 ? 'A' + c : c < 52 ? 'a' + (c - 26) : c < 62 ? '0' + (c - 52) : c == 62 ? '+' : '/');
   }
-  const uint32_t delta =
-      dbeg < n ? b64_stage_span<kStage>(data + data_off[i] + dbeg, min(kB64TileBytes, n - dbeg), stage) : 0u;
+  st.store(stage);
+  const uint32_t delta = st.delta;
   __syncthreads();
   const uint32_t* w = reinterpret_cast<const uint32_t*>(stage);
   uint8_t* t = text + text_off[i];

@@ -12,6 +12,7 @@
 // Multiple devices take contiguous index ranges, one host thread each, with no
 // collective.
 #include <hip/hip_runtime.h>
+#include <hsa/hsa_ext_amd.h>
 #include <fcntl.h>
 #include <pthread.h>
 #include <sched.h>
@@ -942,6 +943,13 @@ class AutoPin {
     }
     return true;
   }
+  // copies from these windows were refused: stage what lies in them from now on
+  // (they stay pinned until retired, so their unpin still follows their copies)
+  void give_up(uintptr_t a, uintptr_t b) {
+    std::lock_guard<std::mutex> g(mu_);
+    for (size_t k = index(a); k <= index(b - 1) && k < win_.size(); ++k)
+      if (win_[k].state == kPinned) win_[k].state = kGivenUp;
+  }
   // the worker will not read below `a` again: windows that end there can go
   void retire_before(uintptr_t a) {
     std::lock_guard<std::mutex> g(mu_);
@@ -962,9 +970,16 @@ class AutoPin {
       if (w.ev) (void)hipEventDestroy(w.ev);
   }
   uint64_t pinned_bytes() const { return pinned_bytes_; }
+  // bytes from a to the end of its window: one H2D may not cross a registration
+  // (HIP refuses a copy whose source spans two: "invalid argument")
+  uint64_t room(uintptr_t a) {
+    std::lock_guard<std::mutex> g(mu_);
+    const size_t k = index(a);
+    return k < win_.size() ? win_[k].hi - a : 0;
+  }
 
  private:
-  static constexpr int kPending = 0, kPinned = 1, kFailed = 2, kUnpinned = 3;
+  static constexpr int kPending = 0, kPinned = 1, kFailed = 2, kUnpinned = 3, kGivenUp = 4;
   static constexpr size_t kAhead = 4;
   struct Window {
     uintptr_t lo, hi;
@@ -985,7 +1000,7 @@ class AutoPin {
       // retired windows first: the worker does not read their pages again
       while (unpinned < std::min(retired_, next)) {
         Window& w = win_[unpinned++];
-        if (w.state != kPinned) continue;
+        if (w.state != kPinned && w.state != kGivenUp) continue;
         g.unlock();
         if (w.used && w.ev) (void)hipEventSynchronize(w.ev);  // its last copy has landed
         (void)hipHostUnregister(reinterpret_cast<void*>(w.lo));
@@ -1196,9 +1211,6 @@ int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
         autopin->retire_before(g_lo);  // runs come in address order: nothing below this group is read again
         direct = cursor >= runs.size() * kDirectMinRun && autopin->covered(g_lo, g_hi);
       }
-      const bool single = !direct && hdr + cursor <= w.pin_bytes;
-      const uint64_t data_off = single ? hdr : w.hdr_cap;
-      uint8_t* h_header = nullptr;
       for (Run& r : runs) r.avail = 0;
       if (direct) {
         // A batch's copies start only once the previous direct batch's have
@@ -1215,23 +1227,52 @@ int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
         // GiB/s, profiles/r02/registered_trace/piece_sweep/); ordered, whole runs are as fast
         // or faster (50.6 against 49.6-49.8 GiB/s at 4 GiB, direct_ordered/).
         const uint64_t piece = env_u64("LBF_DIRECT_PIECE_MB", 0) << 20;
+        bool refused = false;  // an on-the-fly window HIP cannot copy from (see below)
         for (Run& r : runs) {
           const uint64_t step = piece ? piece : r.len;
-          for (uint64_t at = 0; at < r.len && rc == LBF_OK; at += step)
-            if (!hip_ok(hipMemcpyAsync(s.d_buf + data_off + r.dst + at, job.src.base + r.src + at,
-                                       std::min(step, r.len - at), hipMemcpyHostToDevice, s.stream),
-                        "hipMemcpyAsync(H2D, registered source)"))
+          for (uint64_t at = 0, len = 0; at < r.len && rc == LBF_OK && !refused; at += len) {
+            len = std::min(step, r.len - at);
+            if (autopin)  // on-the-fly windows are separate registrations: one copy per window
+              len = std::min<uint64_t>(len, autopin->room(reinterpret_cast<uintptr_t>(job.src.base + r.src + at)));
+            if (len == 0) {
+              rc = fail(LBF_ERR_INVALID, "on-the-fly pinning: a run outside its windows");
               break;
-          if (rc) break;
+            }
+            const hipError_t e = hipMemcpyAsync(s.d_buf + w.hdr_cap + r.dst + at, job.src.base + r.src + at, len,
+                                                hipMemcpyHostToDevice, s.stream);
+            if (e == hipErrorInvalidValue && autopin) {
+              // HIP lets a window be registered over a range the caller had
+              // pinned itself, then resolves copies in that range to the
+              // caller's (smaller) registration and refuses them at enqueue.
+              // Such a window is given up and this batch staged; the copies
+              // already queued run before the staged ones on the same stream,
+              // which overwrite whatever they wrote.
+              (void)hipGetLastError();
+              refused = true;
+            } else if (!hip_ok(e, "hipMemcpyAsync(H2D, registered source)")) {
+              break;
+            }
+          }
+          if (rc || refused) break;
           r.avail = r.len;
         }
-        if (rc || !hip_ok(hipEventRecord(s.copied, s.stream), "hipEventRecord")) break;
-        if (autopin && !autopin->used(g_lo, g_hi, s.stream)) {
-          rc = fail(LBF_ERR_HIP, "hipEventRecord (on-the-fly pinning)");
-          break;
+        if (rc) break;
+        if (refused) {
+          autopin->give_up(g_lo, g_hi);
+          direct = false;
+          for (Run& r : runs) r.avail = 0;
+        } else {
+          if (!hip_ok(hipEventRecord(s.copied, s.stream), "hipEventRecord")) break;
+          if (autopin && !autopin->used(g_lo, g_hi, s.stream)) {
+            rc = fail(LBF_ERR_HIP, "hipEventRecord (on-the-fly pinning)");
+            break;
+          }
+          prev_direct = cur;
         }
-        prev_direct = cur;
       }
+      const bool single = !direct && hdr + cursor <= w.pin_bytes;
+      const uint64_t data_off = single ? hdr : w.hdr_cap;
+      uint8_t* h_header = nullptr;
       (direct ? w.bytes_direct : w.bytes_staged) += cursor;
       std::vector<bool> cut_short(runs.size(), false);
       size_t first_run = 0;
@@ -1428,14 +1469,39 @@ std::map<uintptr_t, Pin> g_pins;  // lo -> pin, disjoint ranges
 struct PinnedAlloc {
   bool pinned = false;
   uintptr_t base = 0, end = 0;  // end == 0: the extent is unknown
+  uint64_t id = 0;              // HIP's buffer id of the allocation (0: unknown)
 };
 PinnedAlloc pinned_alloc(uintptr_t p) {
   PinnedAlloc out;
+  // The runtime under HIP reports the host base and size of the allocation a
+  // pinned pointer lies in, for hipHostMalloc (an HSA pool allocation) and for
+  // hipHostRegister (locked) memory alike.  hipMemGetAddressRange gives the
+  // size of a hipHostRegister'd range but a null base (measured on the box,
+  // tools/pin_extent_probe.py), so it is only the fallback.
+  hsa_amd_pointer_info_t info{};
+  info.size = sizeof(info);
+  if (hsa_amd_pointer_info(reinterpret_cast<const void*>(p), &info, nullptr, nullptr, nullptr) == HSA_STATUS_SUCCESS &&
+      (info.type == HSA_EXT_POINTER_TYPE_LOCKED || info.type == HSA_EXT_POINTER_TYPE_HSA) && info.hostBaseAddress &&
+      info.sizeInBytes) {
+    const uintptr_t b = reinterpret_cast<uintptr_t>(info.hostBaseAddress);
+    if (b <= p && p - b < info.sizeInBytes) {
+      out.pinned = true;
+      out.base = b;
+      out.end = b + info.sizeInBytes;
+      return out;
+    }
+  }
   hipPointerAttribute_t attr{};
   out.pinned = hipPointerGetAttributes(&attr, reinterpret_cast<void*>(p)) == hipSuccess &&
                attr.type == hipMemoryTypeHost;
   (void)hipGetLastError();  // pageable memory is an error to that query
   if (!out.pinned) return out;
+  // One id per allocation or registration: two addresses with the same id lie
+  // in one allocation, and so does every byte between them.
+  unsigned long long id = 0;
+  if (hipPointerGetAttribute(&id, HIP_POINTER_ATTRIBUTE_BUFFER_ID, reinterpret_cast<hipDeviceptr_t>(p)) == hipSuccess)
+    out.id = id;
+  (void)hipGetLastError();
   const uintptr_t dev = reinterpret_cast<uintptr_t>(attr.devicePointer);
   for (const uintptr_t q : {p, dev}) {
     hipDeviceptr_t b = nullptr;
@@ -1593,11 +1659,12 @@ extern "C" int lbf_host_register(lbf_ctx* ctx, const void* ptr, uint64_t len) {
     // buffer pinned whole by the caller need not end on a page boundary).
     const uint64_t uend = a + len;
     const PinnedAlloc first = pinned_alloc(a), last = pinned_alloc(uend - 1);
-    if (first.pinned && first.end && first.base <= a && uend <= first.end) {
+    if ((first.pinned && first.end && first.base <= a && uend <= first.end) ||
+        (first.pinned && last.pinned && first.id && first.id == last.id)) {
       ctx->regs.push_back(r);
       return (int)LBF_OK;
     }
-    if (first.pinned && !first.end)
+    if (first.pinned && !first.end && !first.id)
       return fail(LBF_ERR_INVALID,
                   "lbf_host_register: range is pinned already, but HIP does not report the extent of the pinned "
                   "allocation holding it, so it cannot be shown to cover the range");

@@ -179,13 +179,12 @@ int launch_chunks(const ChunkParams& p, hipStream_t stream) {
   return LBF_OK;
 }
 
-// grid.x = chunks x tiles, in launches of at most 2^22 workgroups (a chunk's
-// tiles are never split across launches)
+// grid = (tiles, chunks), in launches of at most 65,535 chunks (grid.y)
 template <class F>
 static int b64_tiled_launch(uint32_t n, uint32_t tiles, F launch) {
-  const uint32_t per = std::max(1u, (1u << 22) / tiles);
-  for (uint32_t c0 = 0; c0 < n; c0 += per) {
-    launch(dim3(std::min(per, n - c0) * tiles), c0);
+  constexpr uint32_t kPer = 65535;
+  for (uint32_t c0 = 0; c0 < n; c0 += kPer) {
+    launch(dim3(tiles, std::min(kPer, n - c0)), c0);
     LBF_HIP_TRY(hipGetLastError());
   }
   return LBF_OK;
