@@ -186,11 +186,87 @@ __device__ __forceinline__ bool b64_canon_groups(uint32_t len, uint32_t* groups)
   return true;
 }
 
-// blockIdx.x = tile, blockIdx.y = chunk - chunk0.  Chunk i's text is
+// One tile of the one-pass decode from its text in LDS (sb, from byte
+// `delta`): lane u < 216 builds and stores bytes [16u, 16u + 16) of the tile.
+// Returns true when the lane saw a character that breaks the layout.
+__device__ __forceinline__ bool b64_decode_tile(const uint8_t* sb, uint32_t delta, const uint8_t* tab, uint32_t tile,
+                                                uint32_t groups, uint32_t len, uint64_t want, uint32_t limit,
+                                                uint8_t* o) {
+  if (threadIdx.x >= kB64TileBytes / 16) return false;
+  // Bytes [16u, 16u + 16) of the tile come from its groups g0 .. g0 + 5, whose
+  // characters lie in [c0, c0 + 25): 24 characters and at most one separator,
+  // after group 17 - r0 of the window when r0 >= 12.  One window of eight
+  // aligned dwords holds them; each group's four characters are cut out of it
+  // with v_alignbyte (no divergent branch: groups past the chunk's end are
+  // decoded from whatever lies there and masked below).
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(sb);
+  const uint32_t b0 = 16 * threadIdx.x, g0 = b0 / 3, phase = b0 - 3 * g0;
+  const uint32_t l0 = g0 / 18, r0 = g0 - 18 * l0;
+  const uint32_t c0 = delta + 4 * g0 + l0, sh0 = c0 & 3u;
+  const uint32_t* wb = w + (c0 >> 2);
+  uint32_t win[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) win[k] = wb[k];
+  const uint32_t gbase = tile * kB64TileGroups + g0;  // the chunk's index of group g0
+  bool bad = false;
+  uint32_t x[6];
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    const uint32_t sep = r0 + j >= 18 ? 1u : 0u;
+    const uint32_t off = sh0 + sep;  // 0..4: this group's offset from dword j of the window
+    const uint32_t lo = off >= 4 ? win[j + 1] : win[j], hi = off >= 4 ? win[j + 2] : win[j + 1];
+    const uint32_t c = __builtin_amdgcn_alignbyte(hi, lo, off & 3u);
+    const uint32_t s0 = tab[c & 255], s1 = tab[(c >> 8) & 255], s2 = tab[(c >> 16) & 255], s3 = tab[c >> 24];
+    const uint32_t gg = gbase + j;
+    // inside the text every character is in the alphabet; the last group's
+    // padding is checked by the kernel
+    const bool inner = ((s0 | s1 | s2 | s3) & ~63u) != 0, head = ((s0 | s1) & ~63u) != 0;
+    bad |= (gg + 1 < groups && inner) || (gg + 1 == groups && head);
+    x[j] = ((s0 & 63) << 18) | ((s1 & 63) << 12) | ((s2 & 63) << 6) | (s3 & 63);
+  }
+  // the separator after group 17 - r0 (when in the window): any character outside the alphabet
+  {
+    const uint32_t js = 17 - r0;  // < 6 when r0 >= 12
+    const uint32_t gs = gbase + js;
+    const uint32_t at = (c0 & ~3u) + min(sh0 + 4 * js + 4, 31u);
+    const bool check = r0 >= 12 && 4 * gs + gs / 18 + 4 < len;
+    bad |= check && tab[sb[at]] != kB64Skip;
+  }
+  // the 18 bytes of the six groups, as little-endian words
+  auto by = [&](int j, int k) { return (x[j] >> (16 - 8 * k)) & 255u; };
+  const uint32_t W0 = by(0, 0) | by(0, 1) << 8 | by(0, 2) << 16 | by(1, 0) << 24;
+  const uint32_t W1 = by(1, 1) | by(1, 2) << 8 | by(2, 0) << 16 | by(2, 1) << 24;
+  const uint32_t W2 = by(2, 2) | by(3, 0) << 8 | by(3, 1) << 16 | by(3, 2) << 24;
+  const uint32_t W3 = by(4, 0) | by(4, 1) << 8 | by(4, 2) << 16 | by(5, 0) << 24;
+  const uint32_t W4 = by(5, 1) | by(5, 2) << 8;
+  uint4 v = make_uint4(__builtin_amdgcn_alignbyte(W1, W0, phase), __builtin_amdgcn_alignbyte(W2, W1, phase),
+                       __builtin_amdgcn_alignbyte(W3, W2, phase), __builtin_amdgcn_alignbyte(W4, W3, phase));
+  const uint64_t pos = (uint64_t)tile * kB64TileBytes + b0;
+  if (pos < limit) {
+    if (pos + 16 > want) {  // the decoded bytes end inside this block: zero the rest of the slot
+      uint32_t ws[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int m = 0; m < 16; ++m)
+        if (pos + m >= want) ws[m >> 2] &= ~(255u << (8 * (m & 3)));
+      v = make_uint4(ws[0], ws[1], ws[2], ws[3]);
+    }
+    b64_put_block(o, pos, limit, v);
+  }
+  return bad;
+}
+
+// Tiles per workgroup: a workgroup takes kB64TilesPerGroup consecutive tiles
+// of its chunk and double-buffers them in LDS, so the next tile's loads are in
+// flight while it decodes (or encodes) the current one: one barrier per tile,
+// and a CU's resident workgroups keep loads outstanding through their compute.
+constexpr uint32_t kB64TilesPerGroup = 4;
+
+// blockIdx.x = group of tiles, blockIdx.y = chunk - chunk0.  Chunk i's text is
 // text[text_off[i] .. + text_len[i]); its decoded bytes go to
 // out[out_off[i] .. + cap[i]): bytes [0, min(decoded, cap)) decoded, the rest
 // of the slot zeroed, so a short text never leaves stale device bytes in the
 // caller's slot.  sizes[i] = min(decoded, cap[i]), over[i] = decoded > cap[i].
+// `tiles` = the tiles that cover the chunk with the most (text or slot).
 __global__ void __launch_bounds__(kB64Threads) b64_decode_canon_kernel(const uint8_t* __restrict__ text,
                                                                        const uint64_t* __restrict__ text_off,
                                                                        const uint32_t* __restrict__ text_len,
@@ -201,25 +277,35 @@ __global__ void __launch_bounds__(kB64Threads) b64_decode_canon_kernel(const uin
                                                                        uint8_t* __restrict__ over,
                                                                        uint8_t* __restrict__ redo, uint32_t tiles,
                                                                        uint32_t chunk0) {
-  // the span, its phase, and slack for the last lane's 32-byte window read
+  // a tile's span, its phase, and slack for the last lane's 32-byte window read
   constexpr uint32_t kStage = (kB64TileText + 15 + 15) / 16 + 2;
   static_assert(kStage <= 2 * kB64Threads, "two blocks per lane at most");
-  __shared__ uint4 stage[kStage];
+  __shared__ uint4 stage[2][kStage];
   __shared__ uint8_t tab[256];
   __shared__ uint32_t last_shared;
-  const uint32_t i = chunk0 + blockIdx.y, tile = blockIdx.x;
+  const uint32_t i = chunk0 + blockIdx.y, t0 = blockIdx.x * kB64TilesPerGroup;
   const uint32_t len = text_len[i];
   uint32_t groups = 0;
   if (!b64_canon_groups(len, &groups)) {  // the whole workgroup leaves: no barrier below is reached
-    if (tile == 0 && threadIdx.x == 0) redo[i] = 1;
+    if (t0 == 0 && threadIdx.x == 0) redo[i] = 1;
     return;
   }
   const uint32_t limit = cap[i];
-  const uint32_t tbeg = tile * kB64TileText, obeg = tile * kB64TileBytes;
-  if (tbeg >= len && obeg >= limit && tile != 0) return;  // past this chunk's text and slot (the whole workgroup)
+  // the tiles this chunk has: its text's and its slot's (at least one, for the sizes)
+  const uint32_t own = max(1u, max((len + kB64TileText - 1) / kB64TileText,
+                                   (limit + kB64TileBytes - 1) / kB64TileBytes));
+  if (t0 >= own) return;  // the whole workgroup
+  const uint32_t t1 = min(own, t0 + kB64TilesPerGroup);
   const uint8_t* t = text + text_off[i];
+  uint8_t* o = out + out_off[i];
   B64Stage st;
-  if (tbeg < len) st.load(t + tbeg, min(kB64TileText, len - tbeg));
+  auto load = [&](uint32_t tile) {
+    const uint32_t tbeg = tile * kB64TileText;
+    st.blocks = 0;
+    st.delta = 0;
+    if (tbeg < len) st.load(t + tbeg, min(kB64TileText, len - tbeg));
+  };
+  load(t0);
   tab[threadIdx.x] = (uint8_t)b64_value(threadIdx.x);
   if (threadIdx.x == 0) {
     // the last group -- "xxxx", "xxx=" or "xx==" -- sets the decoded length
@@ -232,78 +318,26 @@ __global__ void __launch_bounds__(kB64Threads) b64_decode_canon_kernel(const uin
       bad = c3 == kB64Skip || c2 == kB64Skip || (c2 == kB64Eq && c3 != kB64Eq);
     }
     last_shared = last;
-    if (tile == 0) {
+    if (t0 == 0) {
       const uint64_t want = groups ? 3ull * (groups - 1) + last : 0;
       sizes[i] = (uint32_t)min<uint64_t>(want, limit);
       over[i] = want > limit ? 1 : 0;
       if (bad) redo[i] = 1;
     }
   }
-  st.store(stage);
-  const uint32_t delta = st.delta;
+  st.store(stage[0]);
+  uint32_t delta = st.delta;
   __syncthreads();
   const uint64_t want = groups ? 3ull * (groups - 1) + last_shared : 0;
-  if (tbeg >= len && obeg >= limit) return;  // tile 0 of an empty chunk with an empty slot
-  const uint32_t* w = reinterpret_cast<const uint32_t*>(stage);
-  const uint8_t* sb = reinterpret_cast<const uint8_t*>(stage);
   bool bad = false;
-  if (threadIdx.x < kB64TileBytes / 16) {
-    // Bytes [16u, 16u + 16) of the tile come from its groups g0 .. g0 + 5, whose
-    // characters lie in [c0, c0 + 25): 24 characters and at most one
-    // separator, after group 17 - r0 of the window when r0 >= 12.  One window
-    // of eight aligned dwords holds them; each group's four characters are cut
-    // out of it with v_alignbyte (no divergent branch: groups past the chunk's
-    // end are decoded from whatever lies there and masked below).
-    const uint32_t b0 = 16 * threadIdx.x, g0 = b0 / 3, phase = b0 - 3 * g0;
-    const uint32_t l0 = g0 / 18, r0 = g0 - 18 * l0;
-    const uint32_t c0 = delta + 4 * g0 + l0, sh0 = c0 & 3u;
-    const uint32_t* wb = w + (c0 >> 2);
-    uint32_t win[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) win[k] = wb[k];
-    const uint32_t gbase = tile * kB64TileGroups + g0;  // the chunk's index of group g0
-    uint32_t x[6];
-#pragma unroll
-    for (int j = 0; j < 6; ++j) {
-      const uint32_t sep = r0 + j >= 18 ? 1u : 0u;
-      const uint32_t o = sh0 + sep;  // 0..4: this group's offset from dword j of the window
-      const uint32_t lo = o >= 4 ? win[j + 1] : win[j], hi = o >= 4 ? win[j + 2] : win[j + 1];
-      const uint32_t c = __builtin_amdgcn_alignbyte(hi, lo, o & 3u);
-      const uint32_t s0 = tab[c & 255], s1 = tab[(c >> 8) & 255], s2 = tab[(c >> 16) & 255], s3 = tab[c >> 24];
-      const uint32_t gg = gbase + j;
-      // inside the text every character is in the alphabet; the last group's
-      // padding was checked above
-      const bool inner = ((s0 | s1 | s2 | s3) & ~63u) != 0, head = ((s0 | s1) & ~63u) != 0;
-      bad |= (gg + 1 < groups && inner) || (gg + 1 == groups && head);
-      x[j] = ((s0 & 63) << 18) | ((s1 & 63) << 12) | ((s2 & 63) << 6) | (s3 & 63);
-    }
-    // the separator after group 17 - r0 (when in the window): any character outside the alphabet
-    {
-      const uint32_t js = 17 - r0;  // < 6 when r0 >= 12
-      const uint32_t gs = gbase + js;
-      const uint32_t at = (c0 & ~3u) + min(sh0 + 4 * js + 4, 31u);
-      const bool check = r0 >= 12 && 4 * gs + gs / 18 + 4 < len;
-      bad |= check && tab[sb[at]] != kB64Skip;
-    }
-    // the 18 bytes of the six groups, as little-endian words
-    auto by = [&](int j, int k) { return (x[j] >> (16 - 8 * k)) & 255u; };
-    const uint32_t W0 = by(0, 0) | by(0, 1) << 8 | by(0, 2) << 16 | by(1, 0) << 24;
-    const uint32_t W1 = by(1, 1) | by(1, 2) << 8 | by(2, 0) << 16 | by(2, 1) << 24;
-    const uint32_t W2 = by(2, 2) | by(3, 0) << 8 | by(3, 1) << 16 | by(3, 2) << 24;
-    const uint32_t W3 = by(4, 0) | by(4, 1) << 8 | by(4, 2) << 16 | by(5, 0) << 24;
-    const uint32_t W4 = by(5, 1) | by(5, 2) << 8;
-    uint4 v = make_uint4(__builtin_amdgcn_alignbyte(W1, W0, phase), __builtin_amdgcn_alignbyte(W2, W1, phase),
-                         __builtin_amdgcn_alignbyte(W3, W2, phase), __builtin_amdgcn_alignbyte(W4, W3, phase));
-    const uint64_t pos = obeg + b0;
-    if (pos < limit) {
-      if (pos + 16 > want) {  // the decoded bytes end inside this block: zero the rest of the slot
-        uint32_t ws[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int m = 0; m < 16; ++m)
-          if (pos + m >= want) ws[m >> 2] &= ~(255u << (8 * (m & 3)));
-        v = make_uint4(ws[0], ws[1], ws[2], ws[3]);
-      }
-      b64_put_block(out + out_off[i], pos, limit, v);
+  for (uint32_t tile = t0; tile < t1; ++tile) {
+    const uint32_t buf = (tile - t0) & 1u;
+    if (tile + 1 < t1) load(tile + 1);  // in flight while this tile decodes
+    bad |= b64_decode_tile(reinterpret_cast<const uint8_t*>(stage[buf]), delta, tab, tile, groups, len, want, limit, o);
+    if (tile + 1 < t1) {
+      st.store(stage[buf ^ 1u]);  // that buffer's last reader was the previous tile, before the last barrier
+      delta = st.delta;
+      __syncthreads();
     }
   }
   if (bad) redo[i] = 1;  // every writer stores the same 1
@@ -461,41 +495,17 @@ __host__ __device__ constexpr uint64_t b64_put_length(uint64_t size) {
   return 4 * (size / 3) + (size % 3 ? 4 : 0) + size / 3 / 18;
 }
 
-// blockIdx.x = tile, blockIdx.y = chunk - chunk0: tile k of chunk i encodes bytes
-// [3456k, +3456) into text [4672k, +4672) (clipped to the chunk).  Each lane
-// writes one 16-byte block of the text: characters [p, p + 16) of a line lie
-// in at most five consecutive "words" of the line's character stream, where
-// word e of line l is group e's four characters for e < 18 and, past the
-// line's end, the next line's group e - 18 shifted one byte right behind the
-// separator; v_alignbyte cuts the block out of them.
-__global__ void __launch_bounds__(kB64Threads) b64_encode_kernel(const uint8_t* __restrict__ data,
-                                                                 const uint64_t* __restrict__ data_off,
-                                                                 const uint32_t* __restrict__ size,
-                                                                 uint8_t* __restrict__ text,
-                                                                 const uint64_t* __restrict__ text_off, uint32_t tiles,
-                                                                 uint32_t chunk0) {
-  // the span, its phase, and slack for the group reads of the last window
-  // (computed for every word, used only inside the tile)
-  constexpr uint32_t kStage = (kB64TileBytes + 15) / 16 + 4;
-  static_assert(kStage <= 2 * kB64Threads, "two blocks per lane at most");
-  __shared__ uint4 stage[kStage];
-  __shared__ uint8_t alpha[64];
-  const uint32_t i = chunk0 + blockIdx.y, tile = blockIdx.x;
-  const uint32_t n = size[i], full = n / 3, rest = n % 3;
-  const uint64_t tl = b64_put_length(n);
-  const uint32_t tbeg = tile * kB64TileText, dbeg = tile * kB64TileBytes;
-  if (tbeg >= tl) return;  // the whole workgroup: no barrier below is reached
-  B64Stage st;
-  if (dbeg < n) st.load(data + data_off[i] + dbeg, min(kB64TileBytes, n - dbeg));
-  if (threadIdx.x < 64) {
-    const uint32_t c = threadIdx.x;
-    alpha[c] = (uint8_t)(c < 26 ? 'A' + c : c < 52 ? 'a' + (c - 26) : c < 62 ? '0' + (c - 52) : c == 62 ? '+' : '/');
-  }
-  st.store(stage);
-  const uint32_t delta = st.delta;
-  __syncthreads();
-  const uint32_t* w = reinterpret_cast<const uint32_t*>(stage);
-  uint8_t* t = text + text_off[i];
+// One tile of the encode from its bytes in LDS (sb, from byte `delta`): lane
+// v writes characters [16v, 16v + 16) of the tile's text.  Characters [p, p +
+// 16) of a line lie in at most five consecutive "words" of the line's
+// character stream, where word e of line l is group e's four characters for
+// e < 18 and, past the line's end, the next line's group e - 18 shifted one
+// byte right behind the separator; v_alignbyte cuts the block out of them.
+__device__ __forceinline__ void b64_encode_tile(const uint8_t* sb, uint32_t delta, const uint8_t* alpha,
+                                                uint32_t tile, uint32_t full, uint32_t rest, uint64_t tl,
+                                                uint8_t* t) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(sb);
+  const uint32_t tbeg = tile * kB64TileText;
   // group gl of the tile as its four characters, first character in the low byte
   auto chars = [&](uint32_t gl) -> uint32_t {
     const uint32_t gg = tile * kB64TileGroups + gl;
@@ -527,6 +537,56 @@ __global__ void __launch_bounds__(kB64Threads) b64_encode_kernel(const uint8_t* 
     const uint4 out = make_uint4(__builtin_amdgcn_alignbyte(E[1], E[0], sh), __builtin_amdgcn_alignbyte(E[2], E[1], sh),
                                  __builtin_amdgcn_alignbyte(E[3], E[2], sh), __builtin_amdgcn_alignbyte(E[4], E[3], sh));
     b64_put_block(t, pos, tl, out);
+  }
+}
+
+// blockIdx.x = group of tiles, blockIdx.y = chunk - chunk0: tile k of chunk i
+// encodes bytes [3456k, +3456) into text [4672k, +4672) (clipped to the
+// chunk), kB64TilesPerGroup tiles per workgroup, double-buffered as the decode.
+__global__ void __launch_bounds__(kB64Threads) b64_encode_kernel(const uint8_t* __restrict__ data,
+                                                                 const uint64_t* __restrict__ data_off,
+                                                                 const uint32_t* __restrict__ size,
+                                                                 uint8_t* __restrict__ text,
+                                                                 const uint64_t* __restrict__ text_off, uint32_t tiles,
+                                                                 uint32_t chunk0) {
+  // a tile's span, its phase, and slack for the group reads of the last window
+  // (computed for every word, used only inside the tile)
+  constexpr uint32_t kStage = (kB64TileBytes + 15) / 16 + 4;
+  static_assert(kStage <= 2 * kB64Threads, "two blocks per lane at most");
+  __shared__ uint4 stage[2][kStage];
+  __shared__ uint8_t alpha[64];
+  const uint32_t i = chunk0 + blockIdx.y, t0 = blockIdx.x * kB64TilesPerGroup;
+  const uint32_t n = size[i], full = n / 3, rest = n % 3;
+  const uint64_t tl = b64_put_length(n);
+  const uint32_t own = (uint32_t)((tl + kB64TileText - 1) / kB64TileText);
+  if (t0 >= own) return;  // the whole workgroup: no barrier below is reached
+  const uint32_t t1 = min(own, t0 + kB64TilesPerGroup);
+  const uint8_t* d = data + data_off[i];
+  uint8_t* t = text + text_off[i];
+  B64Stage st;
+  auto load = [&](uint32_t tile) {
+    const uint32_t dbeg = tile * kB64TileBytes;
+    st.blocks = 0;
+    st.delta = 0;
+    if (dbeg < n) st.load(d + dbeg, min(kB64TileBytes, n - dbeg));
+  };
+  load(t0);
+  if (threadIdx.x < 64) {
+    const uint32_t c = threadIdx.x;
+    alpha[c] = (uint8_t)(c < 26 ? 'A' + c : c < 52 ? 'a' + (c - 26) : c < 62 ? '0' + (c - 52) : c == 62 ? '+' : '/');
+  }
+  st.store(stage[0]);
+  uint32_t delta = st.delta;
+  __syncthreads();
+  for (uint32_t tile = t0; tile < t1; ++tile) {
+    const uint32_t buf = (tile - t0) & 1u;
+    if (tile + 1 < t1) load(tile + 1);  // in flight while this tile encodes
+    b64_encode_tile(reinterpret_cast<const uint8_t*>(stage[buf]), delta, alpha, tile, full, rest, tl, t);
+    if (tile + 1 < t1) {
+      st.store(stage[buf ^ 1u]);
+      delta = st.delta;
+      __syncthreads();
+    }
   }
 }
 

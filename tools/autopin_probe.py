@@ -53,7 +53,11 @@ def main():
     a = ap.parse_args()
     sizes = [int(x) for x in a.sizes.split(",")]
     page = os.sysconf("SC_PAGESIZE")
-    big = np.random.default_rng(7).integers(0, 256, size=max(sizes) << 20, dtype=np.uint8)
+    # page-aligned (mmap), so pieces of whole pages never share one (lbf_host_register pins whole pages)
+    import mmap
+    _mm = mmap.mmap(-1, max(sizes) << 20)
+    big = np.frombuffer(_mm, dtype=np.uint8)
+    big[:] = np.random.default_rng(7).integers(0, 256, size=big.size, dtype=np.uint8)
     out = {"piece_mib": a.piece_mib, "gibs": {}, "pin": {}}
     with ChunkHasher(device_mask=1) as h:
         for mib in sizes:
@@ -82,6 +86,7 @@ def main():
                 done = [threading.Event() for _ in views]
 
                 def helper():
+                  try:
                     for k, v in enumerate(views):
                         h.register_host(v)
                         ready[k].set()
@@ -90,11 +95,14 @@ def main():
                             h.unregister_host(views[k - 1])
                     done[-1].wait()
                     h.unregister_host(views[-1])
+                  except Exception as e:  # the main thread times out on ready[] and reports
+                    print(f"helper: {e}", file=sys.stderr, flush=True)
                 th = threading.Thread(target=helper)
                 th.start()
                 last = None
                 for k, v in enumerate(views):
-                    ready[k].wait()
+                    if not ready[k].wait(timeout=60):
+                        raise RuntimeError("the pinning helper stopped")
                     last = h.hash_chunks(v, *tabs[k])
                     done[k].set()
                 th.join()
