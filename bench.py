@@ -553,6 +553,18 @@ def e2e_leg(host_data, cs, dev, world):
     try:
         attempt(lambda: h.hash_chunks(host_data, offs, sizes), "warm pass")  # sizes the staging to this job
         pag_agg, pag_own, d_pag = passes(h)
+        # the same pageable memory through the staging memcpy (LBF_AUTOPIN=0): the
+        # route every pageable job took before round 5 pinned large ones on the fly
+        old = os.environ.get("LBF_AUTOPIN")
+        os.environ["LBF_AUTOPIN"] = "0"
+        try:
+            attempt(lambda: h.hash_chunks(host_data, offs, sizes), "warm staged pass")
+            stg_agg, stg_own, d_stg = passes(h)
+        finally:
+            if old is None:
+                os.environ.pop("LBF_AUTOPIN", None)
+            else:
+                os.environ["LBF_AUTOPIN"] = old
         placement = attempt(lambda: h.worker_info(0), "worker_info") or placement
         t0 = time.perf_counter()
         registered = attempt(lambda: h.register_host(host_data) or True, "lbf_host_register") or False
@@ -568,7 +580,8 @@ def e2e_leg(host_data, cs, dev, world):
                 except Exception as e:
                     err.append(f"lbf_host_unregister: {type(e).__name__}: {e}")
             h.close()
-    return {"pageable_agg": pag_agg, "pageable_own": pag_own, "registered_agg": reg_agg,
+    return {"pageable_agg": pag_agg, "pageable_own": pag_own, "staged_agg": stg_agg, "staged_own": stg_own,
+            "staged_equal": d_stg is not None and bool(np.array_equal(d_stg, d_pag)), "registered_agg": reg_agg,
             "registered_own": reg_own, "register_s": reg_s,
             "direct_fraction": (s1["direct"] - s0["direct"]) / max(1, 3 * host_data.size),
             "digests": d_pag, "registered_equal": d_reg is not None and bool(np.array_equal(d_reg, d_pag)),
@@ -829,14 +842,19 @@ def main():
         r = e2e_leg(host, cs, dev, world)
         del host
         ok = int(np.array_equal(r["digests"], digests[:n_slice]) and r["registered_equal"])
-        g = {k: gather_floats(r[k], world) for k in ("pageable_own", "registered_own", "register_s")}
+        g = {k: gather_floats(r[k], world) for k in ("pageable_own", "staged_own", "registered_own", "register_s")}
         e2e_multi = {
             "what": f"every rank hashes the first {slice_bytes / GIB:g} GiB of its shard from host memory at the "
-                    "same moment through its own lbf_ctx (NUMA-local pinned staging), pageable then registered; "
+                    "same moment through its own lbf_ctx (NUMA-local pinned staging), pageable (pinned on the fly), "
+                    "pageable through the staging memcpy, then registered; "
                     "best of 3 synchronized passes",
             "bytes_per_rank": slice_bytes, "chunk_size": cs,
             "pageable": {"aggregate_gibs": round(r["pageable_agg"], 3),
-                         "per_rank_gibs": [round(x, 3) for x in g["pageable_own"]]},
+                         "per_rank_gibs": [round(x, 3) for x in g["pageable_own"]],
+                         "route": "pinned on the fly for the job (lbf_capi.cpp AutoPin, the default)"},
+            "staged": {"aggregate_gibs": round(r["staged_agg"], 3),
+                       "per_rank_gibs": [round(x, 3) for x in g["staged_own"]],
+                       "route": "the staging memcpy (LBF_AUTOPIN=0), the pre-round-5 route"},
             "registered": {"aggregate_gibs": round(r["registered_agg"], 3),
                            "per_rank_gibs": [round(x, 3) for x in g["registered_own"]],
                            "register_s_per_rank": [round(x, 4) for x in g["register_s"]],
@@ -951,6 +969,10 @@ def main():
                 r = e2e_leg(host_file, cs, dev, 1)
                 del host_file
                 out["e2e_host_to_host_gibs"] = round(r["pageable_own"], 3)
+                out["e2e_route"] = ("pageable memory pinned on the fly for the job (lbf_capi.cpp AutoPin, the "
+                                    "default since round 5; DESIGN.md §9 item 6)")
+                out["e2e_staged"] = {"gibs": round(r["staged_own"], 3), "parity": r["staged_equal"],
+                                     "route": "the same pageable memory through the staging memcpy (LBF_AUTOPIN=0)"}
                 out["e2e_bytes"] = file_bytes
                 out["e2e_parity"] = bool(np.array_equal(r["digests"], digests))
                 out["e2e_staging"] = r["placement"]

@@ -891,24 +891,66 @@ constexpr uint64_t kJoinGap = 4096;
 // knob) caps the job size that goes direct; by default every size does.
 constexpr uint64_t kDirectMinRun = 1ull << 20;
 
-// Pinning a large pageable job on the fly (LBF_AUTOPIN=1, an A/B knob, off by
-// default).  A pageable job crosses host DRAM three times on
-// the staged route (the caller's write, the staging memcpy's read and write,
-// the DMA's read) and its rate moves with the box's memcpy; a registered one
-// crosses it once (§3).  Here a helper thread pins the job's address span in
-// windows of LBF_AUTOPIN_MB (256 MiB) ahead of the worker, at most
-// kAhead windows past the one being copied; a group whose bytes lie in pinned
-// windows goes the direct route, and each window is unpinned once the worker
-// has moved past it and its last copy has landed (an event recorded after that
-// copy).  A window HIP refuses to pin (pinned elsewhere) stays on the staged route.
+// Pinning a large pageable job on the fly (on by default
+// since round 5, LBF_AUTOPIN=0 turns it off).  A pageable job crosses host DRAM
+// three times on the staged route (the caller's write, the staging memcpy's
+// read and write, the DMA's read) and its rate moves with the box's memcpy; a
+// registered one crosses it once (§3).  On this ROCm, hipHostRegister of a
+// whole 4 GiB job costs about 0.1 ms (tools/autopin_probe.py), so by default
+// the job's address span is registered in one piece before its first copy and
+// unregistered after its last (measured against the staging memcpy on one box,
+// profiles/r05/autopin/: 64 MiB 14.2 against 13.0, 1 GiB 45.2 against 41.8,
+// 4 GiB 50.7 against 49.6 GiB/s).  LBF_AUTOPIN_MB=W instead pins windows of W
+// MiB from a helper thread, at most kAhead windows ahead of the copies, and
+// unpins each once the worker has moved past it and its last copy has landed
+// (an event recorded after that copy); that form measured slower at 4 GiB
+// (46.8) and stays an A/B knob.  A window HIP refuses to pin (pinned
+// elsewhere) stays on the staged route, and so does a batch whose copy HIP
+// refuses (see worker_run).
+// Spans being pinned on the fly by running jobs, process-wide: two contexts
+// hashing the same pageable buffer at once must not both register it (one's
+// unregister could drop pages the other is still copying from), so a span that
+// overlaps another job's, or a range pinned through lbf_host_register, is staged.
+bool pin_table_overlaps(uintptr_t lo, uintptr_t hi);  // lbf_host_register's table (below)
+std::mutex g_autopin_mu;
+std::map<uintptr_t, uintptr_t> g_autopin;  // lo -> hi of the spans reserved now
+bool reserve_autopin(uintptr_t lo, uintptr_t hi) {
+  std::lock_guard<std::mutex> g(g_autopin_mu);
+  auto next = g_autopin.lower_bound(lo);
+  if ((next != g_autopin.end() && next->first < hi) || (next != g_autopin.begin() && std::prev(next)->second > lo))
+    return false;
+  if (pin_table_overlaps(lo, hi)) return false;
+  g_autopin[lo] = hi;
+  return true;
+}
+void release_autopin(uintptr_t lo) {
+  std::lock_guard<std::mutex> g(g_autopin_mu);
+  g_autopin.erase(lo);
+}
+
 class AutoPin {
  public:
   AutoPin(int device, uintptr_t lo, uintptr_t hi, uint64_t window) : device_(device) {
     const uintptr_t page = (uintptr_t)sysconf(_SC_PAGESIZE);
     lo &= ~(page - 1);
     hi = (hi + page - 1) & ~(page - 1);
-    window = std::max<uint64_t>(page, window / page * page);
+    window = window ? std::max<uint64_t>(page, window / page * page) : hi - lo;  // 0: the span in one piece
     for (uintptr_t a = lo; a < hi; a += window) win_.push_back(Window{a, std::min<uintptr_t>(hi, a + window)});
+    reserved_ = lo < hi && reserve_autopin(lo, hi);
+    span_lo_ = lo;
+    if (!reserved_) {  // another job pins (part of) it, or the caller registered it: staged
+      for (Window& w : win_) w.state = kFailed;
+      win_.resize(std::min<size_t>(win_.size(), 1));
+      return;
+    }
+    if (win_.size() == 1) {  // the whole span at once, on this thread
+      Window& w = win_[0];
+      const hipError_t e = hipHostRegister(reinterpret_cast<void*>(w.lo), w.hi - w.lo, hipHostRegisterPortable);
+      if (e != hipSuccess) (void)hipGetLastError();  // pinned elsewhere, or no memory: the job is staged
+      w.state = e == hipSuccess ? kPinned : kFailed;
+      if (e == hipSuccess) pinned_bytes_ = w.hi - w.lo;
+      return;
+    }
     for (Window& w : win_)
       if (hipEventCreateWithFlags(&w.ev, hipEventDisableTiming) != hipSuccess) {
         (void)hipGetLastError();
@@ -933,6 +975,7 @@ class AutoPin {
   // a group's copies from [a, b) were issued on `stream`: record each window's
   // event behind them (the last recording is the one its unpin waits for)
   bool used(uintptr_t a, uintptr_t b, hipStream_t stream) {
+    if (win_.size() == 1) return true;  // unpinned only after the drain
     std::lock_guard<std::mutex> g(mu_);
     for (size_t k = index(a); k <= index(b - 1) && k < win_.size(); ++k) {
       if (!win_[k].ev || hipEventRecord(win_[k].ev, stream) != hipSuccess) {
@@ -958,6 +1001,16 @@ class AutoPin {
   }
   // every stream drained: unpin whatever is left and stop the helper
   void finish() {
+    if (win_.size() <= 1 && !th_.joinable()) {  // the one-piece form: every copy has landed (drained)
+      if (!win_.empty() && (win_[0].state == kPinned || win_[0].state == kGivenUp)) {
+        (void)hipHostUnregister(reinterpret_cast<void*>(win_[0].lo));
+        (void)hipGetLastError();
+        win_[0].state = kUnpinned;
+      }
+      if (reserved_) release_autopin(span_lo_);
+      reserved_ = false;
+      return;
+    }
     if (!th_.joinable()) return;
     {
       std::lock_guard<std::mutex> g(mu_);
@@ -968,6 +1021,8 @@ class AutoPin {
     th_.join();
     for (Window& w : win_)
       if (w.ev) (void)hipEventDestroy(w.ev);
+    if (reserved_) release_autopin(span_lo_);
+    reserved_ = false;
   }
   uint64_t pinned_bytes() const { return pinned_bytes_; }
   // bytes from a to the end of its window: one H2D may not cross a registration
@@ -1032,6 +1087,8 @@ class AutoPin {
     }
   }
   int device_;
+  bool reserved_ = false;
+  uintptr_t span_lo_ = 0;
   std::vector<Window> win_;
   std::mutex mu_;
   std::condition_variable cv_;
@@ -1121,14 +1178,16 @@ int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
   const uint64_t direct_max_mb = env_u64("LBF_DIRECT_MAX_MB", 0);
   const uint64_t direct_max = direct_max_mb ? direct_max_mb << 20 : UINT64_MAX;
   const bool direct_job = job.src.pinned && job_bytes <= direct_max;
-  // LBF_AUTOPIN=1 (A/B knob): pin a large pageable job on the fly (AutoPin above);
-  // only when its runs fill at least half of their address span
+  // Pin a large pageable job on the fly (AutoPin above; LBF_AUTOPIN=0 turns it
+  // off): jobs of LBF_AUTOPIN_MIN_MB (64) and more whose runs fill at least half
+  // of their address span
   std::unique_ptr<AutoPin> autopin;
-  if (!job.src.pinned && !job.src.from_files() && env_long("LBF_AUTOPIN", 0) == 1 && span_hi > span_lo &&
-      job_bytes >= (env_u64("LBF_AUTOPIN_MIN_MB", 256) << 20) && 2 * job_bytes >= span_hi - span_lo) {
+  if (!job.src.pinned && !job.src.from_files() && env_long("LBF_AUTOPIN", 1) == 1 && span_hi > span_lo &&
+      job_bytes >= (env_u64("LBF_AUTOPIN_MIN_MB", 64) << 20) && 2 * job_bytes >= span_hi - span_lo) {
     const uintptr_t b = reinterpret_cast<uintptr_t>(job.src.base);
+    const uint64_t window = env_u64("LBF_AUTOPIN_MB", 0) << 20;  // 0: the whole span in one piece
     try {
-      autopin.reset(new AutoPin(w.device, b + span_lo, b + span_hi, env_u64("LBF_AUTOPIN_MB", 256) << 20));
+      autopin.reset(new AutoPin(w.device, b + span_lo, b + span_hi, window));
     } catch (const std::exception&) {
       autopin.reset();  // no helper thread: the staged route, as without the knob
     }
@@ -1461,6 +1520,12 @@ struct Pin {
 };
 std::mutex g_pin_mu;
 std::map<uintptr_t, Pin> g_pins;  // lo -> pin, disjoint ranges
+
+bool pin_table_overlaps(uintptr_t lo, uintptr_t hi) {
+  std::lock_guard<std::mutex> g(g_pin_mu);
+  auto next = g_pins.lower_bound(lo);
+  return (next != g_pins.end() && next->first < hi) || (next != g_pins.begin() && std::prev(next)->second.hi > lo);
+}
 
 // The pinned host allocation that holds address p, as [base, end), if any.
 // hipMemGetAddressRange resolves host-pinned memory (hipHostMalloc,

@@ -50,8 +50,14 @@ def test_registered_contiguous_hash_and_verify(workers, oracle, monkeypatch):
         exp[flips, 19] ^= 1
         v = h.verify_chunks(buf, offs, sizes, exp)
         assert np.flatnonzero(~v).tolist() == flips
-        # unregistered: the same batch goes through staging, same digests
+        # unregistered: pinned on the fly for the job (the default since round 5),
+        # so the same groups go direct; with LBF_AUTOPIN=0 through staging; same digests
         h.unregister_host(buf)
+        s1 = h.staging_stats()
+        assert np.array_equal(h.hash_chunks(buf, offs, sizes), want)
+        d = _delta(h, s1)
+        assert d["direct"] == buf.size - 12345 and d["staged"] == 12345, d
+        monkeypatch.setenv("LBF_AUTOPIN", "0")
         s1 = h.staging_stats()
         assert np.array_equal(h.hash_chunks(buf, offs, sizes), want)
         d = _delta(h, s1)
@@ -245,16 +251,17 @@ def test_buffer_the_caller_pinned_whole_goes_direct(oracle, hasher, size):
         assert hip.hipHostUnregister(ctypes.c_void_p(base)) == 0
 
 
+@pytest.mark.parametrize("window_mb", [0, 64])
 @pytest.mark.parametrize("mib,piece_pinned", [(600, False), (600, True)])
-def test_on_the_fly_pinning_knob(oracle, hasher, monkeypatch, mib, piece_pinned):
-    """LBF_AUTOPIN=1 (the A/B knob of DESIGN.md §9.6): a large pageable job is
-    pinned window by window while it copies, goes the direct route, and leaves
-    nothing pinned behind; a window HIP refuses (pinned elsewhere) is staged.
-    Digests equal the oracle's either way."""
+def test_on_the_fly_pinning(oracle, hasher, monkeypatch, mib, piece_pinned, window_mb):
+    """A large pageable job is pinned on the fly: its whole
+    span in one registration (the default, window 0) or window by window from a
+    helper thread (LBF_AUTOPIN_MB, an A/B knob).  It goes the direct route and
+    leaves nothing pinned behind; a span or window HIP cannot copy from (part of
+    it pinned elsewhere) is staged.  Digests equal the oracle's either way."""
     import ctypes
     hip = _hip()
-    monkeypatch.setenv("LBF_AUTOPIN", "1")
-    monkeypatch.setenv("LBF_AUTOPIN_MB", "64")
+    monkeypatch.setenv("LBF_AUTOPIN_MB", str(window_mb))
     buf = oracle.synth(95, 0, mib * MIB + 4321, nthreads=8)
     offs, sizes = chunk_table(buf.size, 256 * 1024)
     want = oracle.sha1_batch(buf, offs, sizes, nthreads=8)
@@ -267,9 +274,11 @@ def test_on_the_fly_pinning_knob(oracle, hasher, monkeypatch, mib, piece_pinned)
         s0 = hasher.staging_stats()
         assert np.array_equal(hasher.hash_chunks(buf, offs, sizes), want)
         d = _delta(hasher, s0)
-        assert d["direct"] > buf.size // 2 and d["direct"] + d["staged"] >= buf.size
+        assert d["direct"] + d["staged"] >= buf.size
         if piece_pinned:
             assert d["staged"] > 0
+        if not piece_pinned or window_mb:
+            assert d["direct"] > buf.size // 2, d
     finally:
         if other:
             assert hip.hipHostUnregister(ctypes.c_void_p(other)) == 0
