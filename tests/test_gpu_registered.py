@@ -50,13 +50,24 @@ def test_registered_contiguous_hash_and_verify(workers, oracle, monkeypatch):
         exp[flips, 19] ^= 1
         v = h.verify_chunks(buf, offs, sizes, exp)
         assert np.flatnonzero(~v).tolist() == flips
-        # unregistered: pinned on the fly for the job (the default since round 5),
-        # so the same groups go direct; with LBF_AUTOPIN=0 through staging; same digests
+        # unregistered: pinned on the fly for the job (the default since round 5)
+        # when a worker's share reaches LBF_AUTOPIN_MIN_MB (64 MiB: one worker's
+        # 96 MiB does, two workers' 48 MiB each do not), so the same groups go
+        # direct; with LBF_AUTOPIN=0 through staging; same digests either way
         h.unregister_host(buf)
         s1 = h.staging_stats()
         assert np.array_equal(h.hash_chunks(buf, offs, sizes), want)
         d = _delta(h, s1)
+        if workers == 1:
+            assert d["direct"] == buf.size - 12345 and d["staged"] == 12345, d
+        else:
+            assert d["direct"] == 0 and d["staged"] == buf.size, d
+        monkeypatch.setenv("LBF_AUTOPIN_MIN_MB", "32")
+        s1 = h.staging_stats()
+        assert np.array_equal(h.hash_chunks(buf, offs, sizes), want)
+        d = _delta(h, s1)
         assert d["direct"] == buf.size - 12345 and d["staged"] == 12345, d
+        monkeypatch.delenv("LBF_AUTOPIN_MIN_MB")
         monkeypatch.setenv("LBF_AUTOPIN", "0")
         s1 = h.staging_stats()
         assert np.array_equal(h.hash_chunks(buf, offs, sizes), want)
