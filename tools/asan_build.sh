@@ -17,5 +17,5 @@ $HIPCC $FLAGS -c -o $OUT/asan_capi.o tools/asan_capi.cpp
 # the oracle is the checker, not under test: plain -O2
 gcc -O2 -fPIC -c -o $OUT/sha1_oracle.o oracle/sha1_oracle.c -Ioracle
 $HIPCC --offload-arch=gfx950 $SAN -o $OUT/asan_capi $OUT/asan_capi.o $OUT/lbf_capi.o $OUT/sha1_kernels.o \
-  $OUT/sha1_oracle.o -lpthread
+  $OUT/sha1_oracle.o -lpthread -L/opt/rocm/lib -lhsa-runtime64
 echo "built $OUT/asan_capi"

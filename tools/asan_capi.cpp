@@ -8,7 +8,10 @@
 //   lbf_file_ranges (hash and verify, including a truncated file) and
 //   lbf_files_ranges (verify over 2-4 truncated or missing files)
 //   lbf_verify_encode_b64_batch + lbf_b64_verify_batch (the wire form both ways:
-//   text slots at ragged offsets, some texts cut short)
+//   text slots at ragged offsets, some texts cut short; no byte between slots
+//   written, a short decode's slot tail zeroed)
+// with large pageable jobs pinned on the fly in a third of the contexts, in
+// windows in another third (LBF_AUTOPIN*),
 // against the oracle (oracle/sha1_oracle.c, compiled in as the checker).  Half
 // the jobs read from memory registered with the context, and half the
 // contexts then take three concurrent callers with 24-40 MiB batches (enough
@@ -69,6 +72,12 @@ int main(int argc, char** argv) {
     setenv("LBF_SLOT_MB", std::to_string(slot_mb).c_str(), 1);
     setenv("LBF_TEST_FAULT_GROUP", fault ? std::to_string(uni(0, 3)).c_str() : "-1", 1);
     setenv("LBF_TEST_FAULT_WORKER", std::to_string(uni(0, workers - 1)).c_str(), 1);
+    // on-the-fly pinning of pageable jobs (read per job): off, the whole span, or
+    // 1-2 MiB windows pinned by a helper thread, from 1 MiB of job on
+    const int autopin = (int)uni(0, 2);
+    setenv("LBF_AUTOPIN", autopin ? "1" : "0", 1);
+    setenv("LBF_AUTOPIN_MIN_MB", "1", 1);
+    setenv("LBF_AUTOPIN_MB", autopin == 2 ? std::to_string(uni(1, 2)).c_str() : "0", 1);
     lbf_ctx* ctx = nullptr;
     if (lbf_ctx_create(1, &ctx) != LBF_OK) {
       std::fprintf(stderr, "lbf_ctx_create: %s\n", lbf_last_error());
@@ -213,6 +222,10 @@ int main(int argc, char** argv) {
         for (uint64_t i = 0; i < m && rc == LBF_OK; ++i) CHECK(ev[i] == (bad[i] ? 0 : 1), "encode verdict %lu", (unsigned long)i);
         for (uint64_t k = 0; k < thead; ++k) CHECK(text[k] == '\x01', "text byte %lu before the first slot", (unsigned long)k);
         for (uint64_t k = ttail; k < text.size(); ++k) CHECK(text[k] == '\x01', "text byte %lu after the last slot", (unsigned long)k);
+        for (uint64_t i = 0; i + 1 < m; ++i)  // between slots too: results come back slot by slot
+          for (uint64_t k = toff[i] + tlen[i]; k < toff[i + 1]; ++k)
+            CHECK(text[k] == '\x01', "text byte %lu between slots %lu and %lu", (unsigned long)k, (unsigned long)i,
+                  (unsigned long)i + 1);
         for (uint64_t i = 0; i < m; ++i) {
           dlen[i] = tlen[i];
           if (tlen[i] >= 8 && uni(0, 5) == 0) {  // lose at least one group
@@ -229,7 +242,14 @@ int main(int argc, char** argv) {
                 size[i]);
           if (!cut[i])
             CHECK(memcmp(out.data() + ooff[i], buf.data() + off[i], size[i]) == 0, "decoded bytes %lu", (unsigned long)i);
+          else  // a short decode leaves zeros in the rest of its slot, never stale device bytes
+            for (uint64_t k = dsz[i]; k < size[i]; ++k)
+              CHECK(out[ooff[i] + k] == 0, "slot %lu byte %lu past a short decode", (unsigned long)i, (unsigned long)k);
         }
+        for (uint64_t i = 0; i + 1 < m; ++i)
+          for (uint64_t k = ooff[i] + size[i]; k < ooff[i + 1]; ++k)
+            CHECK(out[k] == 0xA5, "out byte %lu between slots %lu and %lu", (unsigned long)k, (unsigned long)i,
+                  (unsigned long)i + 1);
         for (uint64_t k = 0; k < ohead; ++k) CHECK(out[k] == 0xA5, "out byte %lu before the first slot", (unsigned long)k);
         for (uint64_t k = otail; k < out.size(); ++k) CHECK(out[k] == 0xA5, "out byte %lu after the last slot", (unsigned long)k);
         chunks_checked += (long)(2 * m);
