@@ -105,6 +105,15 @@ constexpr uint32_t kB64TileText = kB64TileLines * 73;    // 4,672 characters
 constexpr uint32_t kB64TileBytes = kB64TileLines * 54;   // 3,456 bytes
 constexpr uint32_t kB64TileGroups = kB64TileLines * 18;  // 1,152 groups
 static_assert(kB64TileText % 16 == 0 && kB64TileBytes % 16 == 0, "tiles of 16-byte blocks");
+// The decode's tile (its output, the bytes, must be whole 16-byte blocks: a
+// multiple of 8 lines; its text tile is read at any phase).  LBF_B64_DEC_LINES
+// and LBF_B64_TILES_PER_GROUP exist for A/B builds (tools/b64_profile.sh).
+#ifndef LBF_B64_DEC_LINES
+#define LBF_B64_DEC_LINES 64
+#endif
+constexpr uint32_t kDecLines = LBF_B64_DEC_LINES;
+constexpr uint32_t kDecText = kDecLines * 73, kDecBytes = kDecLines * 54, kDecGroups = kDecLines * 18;
+static_assert(kDecBytes % 16 == 0 && kDecBytes / 16 <= 256, "a decode tile is at most one 16-byte block per lane");
 typedef uint32_t b64_u32x4 __attribute__((ext_vector_type(4)));  // what the nontemporal builtins take
 
 // Stage global bytes [src, src + len) in LDS as the aligned 16-byte blocks that
@@ -192,7 +201,7 @@ __device__ __forceinline__ bool b64_canon_groups(uint32_t len, uint32_t* groups)
 __device__ __forceinline__ bool b64_decode_tile(const uint8_t* sb, uint32_t delta, const uint8_t* tab, uint32_t tile,
                                                 uint32_t groups, uint32_t len, uint64_t want, uint32_t limit,
                                                 uint8_t* o) {
-  if (threadIdx.x >= kB64TileBytes / 16) return false;
+  if (threadIdx.x >= kDecBytes / 16) return false;
   // Bytes [16u, 16u + 16) of the tile come from its groups g0 .. g0 + 5, whose
   // characters lie in [c0, c0 + 25): 24 characters and at most one separator,
   // after group 17 - r0 of the window when r0 >= 12.  One window of eight
@@ -207,7 +216,7 @@ __device__ __forceinline__ bool b64_decode_tile(const uint8_t* sb, uint32_t delt
   uint32_t win[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) win[k] = wb[k];
-  const uint32_t gbase = tile * kB64TileGroups + g0;  // the chunk's index of group g0
+  const uint32_t gbase = tile * kDecGroups + g0;  // the chunk's index of group g0
   bool bad = false;
   uint32_t x[6];
 #pragma unroll
@@ -241,7 +250,7 @@ __device__ __forceinline__ bool b64_decode_tile(const uint8_t* sb, uint32_t delt
   const uint32_t W4 = by(5, 1) | by(5, 2) << 8;
   uint4 v = make_uint4(__builtin_amdgcn_alignbyte(W1, W0, phase), __builtin_amdgcn_alignbyte(W2, W1, phase),
                        __builtin_amdgcn_alignbyte(W3, W2, phase), __builtin_amdgcn_alignbyte(W4, W3, phase));
-  const uint64_t pos = (uint64_t)tile * kB64TileBytes + b0;
+  const uint64_t pos = (uint64_t)tile * kDecBytes + b0;
   if (pos < limit) {
     if (pos + 16 > want) {  // the decoded bytes end inside this block: zero the rest of the slot
       uint32_t ws[4] = {v.x, v.y, v.z, v.w};
@@ -259,7 +268,10 @@ __device__ __forceinline__ bool b64_decode_tile(const uint8_t* sb, uint32_t delt
 // of its chunk and double-buffers them in LDS, so the next tile's loads are in
 // flight while it decodes (or encodes) the current one: one barrier per tile,
 // and a CU's resident workgroups keep loads outstanding through their compute.
-constexpr uint32_t kB64TilesPerGroup = 4;
+#ifndef LBF_B64_TILES_PER_GROUP
+#define LBF_B64_TILES_PER_GROUP 4
+#endif
+constexpr uint32_t kB64TilesPerGroup = LBF_B64_TILES_PER_GROUP;
 
 // blockIdx.x = group of tiles, blockIdx.y = chunk - chunk0.  Chunk i's text is
 // text[text_off[i] .. + text_len[i]); its decoded bytes go to
@@ -278,7 +290,7 @@ __global__ void __launch_bounds__(kB64Threads) b64_decode_canon_kernel(const uin
                                                                        uint8_t* __restrict__ redo, uint32_t tiles,
                                                                        uint32_t chunk0) {
   // a tile's span, its phase, and slack for the last lane's 32-byte window read
-  constexpr uint32_t kStage = (kB64TileText + 15 + 15) / 16 + 2;
+  constexpr uint32_t kStage = (kDecText + 15 + 15) / 16 + 2;
   static_assert(kStage <= 2 * kB64Threads, "two blocks per lane at most");
   __shared__ uint4 stage[2][kStage];
   __shared__ uint8_t tab[256];
@@ -292,18 +304,18 @@ __global__ void __launch_bounds__(kB64Threads) b64_decode_canon_kernel(const uin
   }
   const uint32_t limit = cap[i];
   // the tiles this chunk has: its text's and its slot's (at least one, for the sizes)
-  const uint32_t own = max(1u, max((len + kB64TileText - 1) / kB64TileText,
-                                   (limit + kB64TileBytes - 1) / kB64TileBytes));
+  const uint32_t own = max(1u, max((len + kDecText - 1) / kDecText,
+                                   (limit + kDecBytes - 1) / kDecBytes));
   if (t0 >= own) return;  // the whole workgroup
   const uint32_t t1 = min(own, t0 + kB64TilesPerGroup);
   const uint8_t* t = text + text_off[i];
   uint8_t* o = out + out_off[i];
   B64Stage st;
   auto load = [&](uint32_t tile) {
-    const uint32_t tbeg = tile * kB64TileText;
+    const uint32_t tbeg = tile * kDecText;
     st.blocks = 0;
     st.delta = 0;
-    if (tbeg < len) st.load(t + tbeg, min(kB64TileText, len - tbeg));
+    if (tbeg < len) st.load(t + tbeg, min(kDecText, len - tbeg));
   };
   load(t0);
   tab[threadIdx.x] = (uint8_t)b64_value(threadIdx.x);
@@ -505,10 +517,10 @@ __device__ __forceinline__ void b64_encode_tile(const uint8_t* sb, uint32_t delt
                                                 uint32_t tile, uint32_t full, uint32_t rest, uint64_t tl,
                                                 uint8_t* t) {
   const uint32_t* w = reinterpret_cast<const uint32_t*>(sb);
-  const uint32_t tbeg = tile * kB64TileText;
+  const uint32_t tbeg = tile * kDecText;
   // group gl of the tile as its four characters, first character in the low byte
   auto chars = [&](uint32_t gl) -> uint32_t {
-    const uint32_t gg = tile * kB64TileGroups + gl;
+    const uint32_t gg = tile * kDecGroups + gl;
     if (gg > full || (gg == full && rest == 0)) return 0u;  // past the text
     const uint32_t b = lds_u32_at(w, delta + 3 * gl);
     uint32_t x = (b & 255u) << 16 | ((b >> 8) & 255u) << 8 | ((b >> 16) & 255u);
@@ -519,7 +531,7 @@ __device__ __forceinline__ void b64_encode_tile(const uint8_t* sb, uint32_t delt
     return (uint32_t)alpha[x >> 18] | (uint32_t)alpha[(x >> 12) & 63] << 8 |
            (rest == 2 ? (uint32_t)alpha[(x >> 6) & 63] : (uint32_t)'=') << 16 | (uint32_t)'=' << 24;
   };
-  for (uint32_t v = threadIdx.x; v < kB64TileText / 16; v += kB64Threads) {
+  for (uint32_t v = threadIdx.x; v < kDecText / 16; v += kB64Threads) {
     const uint32_t p0 = 16 * v;
     const uint64_t pos = tbeg + p0;
     if (pos >= tl) break;

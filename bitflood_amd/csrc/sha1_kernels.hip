@@ -197,7 +197,7 @@ int launch_b64_decode(const B64Launch& b, hipStream_t stream) {
   // two-pass decode of whatever it handed back (a workgroup per chunk, most
   // exit at once)
   const uint32_t tiles = std::max<uint32_t>(
-      1u, std::max((b.max_text_len + kB64TileText - 1) / kB64TileText, (b.max_cap + kB64TileBytes - 1) / kB64TileBytes));
+      1u, std::max((b.max_text_len + kDecText - 1) / kDecText, (b.max_cap + kDecBytes - 1) / kDecBytes));
   if (int rc = b64_tiled_launch(b.n, (tiles + kB64TilesPerGroup - 1) / kB64TilesPerGroup, [&](dim3 grid, uint32_t c0) {
         hipLaunchKernelGGL(b64_decode_canon_kernel, grid, dim3(kB64Threads), 0, stream, b.text, b.text_off, b.text_len,
                            b.out, b.out_off, b.cap, b.sizes, b.over, b.redo, tiles, c0);
