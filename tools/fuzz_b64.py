@@ -103,8 +103,14 @@ def one_case(h, seed):
     offs = np.cumsum([0] + sizes[:-1]).astype(np.uint64)
     v2, enc = h.verify_encode_b64(data, offs, sizes, exp2)
     for k in range(n):
-        if enc[k] != xmlrpc_text(datas[k]) or bool(v2[k]) == bool(bad[k]):
-            return {"chunk": k, "side": "encode", "size": sizes[k]}
+        want = xmlrpc_text(datas[k])
+        if enc[k] != want or bool(v2[k]) == bool(bad[k]):
+            first = next((j for j in range(min(len(want), len(enc[k]))) if enc[k][j] != want[j]), None)
+            return {"chunk": k, "side": "encode", "size": sizes[k], "n": n, "text_len": len(want),
+                    "got_len": len(enc[k]), "first_diff": first,
+                    "got": enc[k][first - 8:first + 24].decode("latin1") if first is not None else None,
+                    "want": want[first - 8:first + 24].decode("latin1") if first is not None else None,
+                    "verdict": bool(v2[k]), "expected_bad": bool(bad[k])}
     return None
 
 
