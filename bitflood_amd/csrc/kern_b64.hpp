@@ -106,10 +106,14 @@ constexpr uint32_t kB64TileBytes = kB64TileLines * 54;   // 3,456 bytes
 constexpr uint32_t kB64TileGroups = kB64TileLines * 18;  // 1,152 groups
 static_assert(kB64TileText % 16 == 0 && kB64TileBytes % 16 == 0, "tiles of 16-byte blocks");
 // The decode's tile (its output, the bytes, must be whole 16-byte blocks: a
-// multiple of 8 lines; its text tile is read at any phase).  LBF_B64_DEC_LINES
-// and LBF_B64_TILES_PER_GROUP exist for A/B builds (tools/b64_profile.sh).
+// multiple of 8 lines; its text tile is read at any phase): 72 lines, 5,256
+// characters -> 3,888 bytes, 243 of the 256 lanes busy (64 lines: 216).  That
+// and eight tiles per workgroup measured 157.6 us per 1,024 x 256 KiB against
+// 171.5-171.8 for 64 lines and four (tools/b64_ab_trace.sh, profiles/r05/b64/).
+// LBF_B64_DEC_LINES, LBF_B64_DEC_TILES_PER_GROUP and LBF_B64_ENC_TILES_PER_GROUP
+// exist for A/B builds (tools/b64_ab_build.sh).
 #ifndef LBF_B64_DEC_LINES
-#define LBF_B64_DEC_LINES 64
+#define LBF_B64_DEC_LINES 72
 #endif
 constexpr uint32_t kDecLines = LBF_B64_DEC_LINES;
 constexpr uint32_t kDecText = kDecLines * 73, kDecBytes = kDecLines * 54, kDecGroups = kDecLines * 18;
@@ -264,14 +268,17 @@ __device__ __forceinline__ bool b64_decode_tile(const uint8_t* sb, uint32_t delt
   return bad;
 }
 
-// Tiles per workgroup: a workgroup takes kB64TilesPerGroup consecutive tiles
+// Tiles per workgroup: a workgroup takes kDecTilesPerGroup (kEncTilesPerGroup) consecutive tiles
 // of its chunk and double-buffers them in LDS, so the next tile's loads are in
 // flight while it decodes (or encodes) the current one: one barrier per tile,
 // and a CU's resident workgroups keep loads outstanding through their compute.
-#ifndef LBF_B64_TILES_PER_GROUP
-#define LBF_B64_TILES_PER_GROUP 4
+#ifndef LBF_B64_DEC_TILES_PER_GROUP
+#define LBF_B64_DEC_TILES_PER_GROUP 8
 #endif
-constexpr uint32_t kB64TilesPerGroup = LBF_B64_TILES_PER_GROUP;
+#ifndef LBF_B64_ENC_TILES_PER_GROUP
+#define LBF_B64_ENC_TILES_PER_GROUP 4  // eight measured 5 % slower for the encode
+#endif
+constexpr uint32_t kDecTilesPerGroup = LBF_B64_DEC_TILES_PER_GROUP, kEncTilesPerGroup = LBF_B64_ENC_TILES_PER_GROUP;
 
 // blockIdx.x = group of tiles, blockIdx.y = chunk - chunk0.  Chunk i's text is
 // text[text_off[i] .. + text_len[i]); its decoded bytes go to
@@ -295,7 +302,7 @@ __global__ void __launch_bounds__(kB64Threads) b64_decode_canon_kernel(const uin
   __shared__ uint4 stage[2][kStage];
   __shared__ uint8_t tab[256];
   __shared__ uint32_t last_shared;
-  const uint32_t i = chunk0 + blockIdx.y, t0 = blockIdx.x * kB64TilesPerGroup;
+  const uint32_t i = chunk0 + blockIdx.y, t0 = blockIdx.x * kDecTilesPerGroup;
   const uint32_t len = text_len[i];
   uint32_t groups = 0;
   if (!b64_canon_groups(len, &groups)) {  // the whole workgroup leaves: no barrier below is reached
@@ -307,7 +314,7 @@ __global__ void __launch_bounds__(kB64Threads) b64_decode_canon_kernel(const uin
   const uint32_t own = max(1u, max((len + kDecText - 1) / kDecText,
                                    (limit + kDecBytes - 1) / kDecBytes));
   if (t0 >= own) return;  // the whole workgroup
-  const uint32_t t1 = min(own, t0 + kB64TilesPerGroup);
+  const uint32_t t1 = min(own, t0 + kDecTilesPerGroup);
   const uint8_t* t = text + text_off[i];
   uint8_t* o = out + out_off[i];
   B64Stage st;
@@ -517,10 +524,10 @@ __device__ __forceinline__ void b64_encode_tile(const uint8_t* sb, uint32_t delt
                                                 uint32_t tile, uint32_t full, uint32_t rest, uint64_t tl,
                                                 uint8_t* t) {
   const uint32_t* w = reinterpret_cast<const uint32_t*>(sb);
-  const uint32_t tbeg = tile * kDecText;
+  const uint32_t tbeg = tile * kB64TileText;
   // group gl of the tile as its four characters, first character in the low byte
   auto chars = [&](uint32_t gl) -> uint32_t {
-    const uint32_t gg = tile * kDecGroups + gl;
+    const uint32_t gg = tile * kB64TileGroups + gl;
     if (gg > full || (gg == full && rest == 0)) return 0u;  // past the text
     const uint32_t b = lds_u32_at(w, delta + 3 * gl);
     uint32_t x = (b & 255u) << 16 | ((b >> 8) & 255u) << 8 | ((b >> 16) & 255u);
@@ -531,7 +538,7 @@ __device__ __forceinline__ void b64_encode_tile(const uint8_t* sb, uint32_t delt
     return (uint32_t)alpha[x >> 18] | (uint32_t)alpha[(x >> 12) & 63] << 8 |
            (rest == 2 ? (uint32_t)alpha[(x >> 6) & 63] : (uint32_t)'=') << 16 | (uint32_t)'=' << 24;
   };
-  for (uint32_t v = threadIdx.x; v < kDecText / 16; v += kB64Threads) {
+  for (uint32_t v = threadIdx.x; v < kB64TileText / 16; v += kB64Threads) {
     const uint32_t p0 = 16 * v;
     const uint64_t pos = tbeg + p0;
     if (pos >= tl) break;
@@ -554,7 +561,7 @@ __device__ __forceinline__ void b64_encode_tile(const uint8_t* sb, uint32_t delt
 
 // blockIdx.x = group of tiles, blockIdx.y = chunk - chunk0: tile k of chunk i
 // encodes bytes [3456k, +3456) into text [4672k, +4672) (clipped to the
-// chunk), kB64TilesPerGroup tiles per workgroup, double-buffered as the decode.
+// chunk), kEncTilesPerGroup tiles per workgroup, double-buffered as the decode.
 __global__ void __launch_bounds__(kB64Threads) b64_encode_kernel(const uint8_t* __restrict__ data,
                                                                  const uint64_t* __restrict__ data_off,
                                                                  const uint32_t* __restrict__ size,
@@ -567,12 +574,12 @@ __global__ void __launch_bounds__(kB64Threads) b64_encode_kernel(const uint8_t* 
   static_assert(kStage <= 2 * kB64Threads, "two blocks per lane at most");
   __shared__ uint4 stage[2][kStage];
   __shared__ uint8_t alpha[64];
-  const uint32_t i = chunk0 + blockIdx.y, t0 = blockIdx.x * kB64TilesPerGroup;
+  const uint32_t i = chunk0 + blockIdx.y, t0 = blockIdx.x * kEncTilesPerGroup;
   const uint32_t n = size[i], full = n / 3, rest = n % 3;
   const uint64_t tl = b64_put_length(n);
   const uint32_t own = (uint32_t)((tl + kB64TileText - 1) / kB64TileText);
   if (t0 >= own) return;  // the whole workgroup: no barrier below is reached
-  const uint32_t t1 = min(own, t0 + kB64TilesPerGroup);
+  const uint32_t t1 = min(own, t0 + kEncTilesPerGroup);
   const uint8_t* d = data + data_off[i];
   uint8_t* t = text + text_off[i];
   B64Stage st;

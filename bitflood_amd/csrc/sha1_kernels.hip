@@ -179,7 +179,7 @@ int launch_chunks(const ChunkParams& p, hipStream_t stream) {
   return LBF_OK;
 }
 
-// grid = (groups of kB64TilesPerGroup tiles, chunks), in launches of at most 65,535 chunks (grid.y)
+// grid = (groups of kDecTilesPerGroup / kEncTilesPerGroup tiles, chunks), in launches of at most 65,535 chunks (grid.y)
 template <class F>
 static int b64_tiled_launch(uint32_t n, uint32_t tiles, F launch) {
   constexpr uint32_t kPer = 65535;
@@ -198,7 +198,7 @@ int launch_b64_decode(const B64Launch& b, hipStream_t stream) {
   // exit at once)
   const uint32_t tiles = std::max<uint32_t>(
       1u, std::max((b.max_text_len + kDecText - 1) / kDecText, (b.max_cap + kDecBytes - 1) / kDecBytes));
-  if (int rc = b64_tiled_launch(b.n, (tiles + kB64TilesPerGroup - 1) / kB64TilesPerGroup, [&](dim3 grid, uint32_t c0) {
+  if (int rc = b64_tiled_launch(b.n, (tiles + kDecTilesPerGroup - 1) / kDecTilesPerGroup, [&](dim3 grid, uint32_t c0) {
         hipLaunchKernelGGL(b64_decode_canon_kernel, grid, dim3(kB64Threads), 0, stream, b.text, b.text_off, b.text_len,
                            b.out, b.out_off, b.cap, b.sizes, b.over, b.redo, tiles, c0);
       }))
@@ -213,7 +213,7 @@ int launch_b64_encode(const uint8_t* data, const uint64_t* data_off, const uint3
                       const uint64_t* text_off, uint32_t n, uint32_t max_size, hipStream_t stream) {
   if (n == 0) return LBF_OK;
   const uint32_t tiles = std::max<uint32_t>(1u, (uint32_t)((b64_put_length(max_size) + kB64TileText - 1) / kB64TileText));
-  return b64_tiled_launch(n, (tiles + kB64TilesPerGroup - 1) / kB64TilesPerGroup, [&](dim3 grid, uint32_t c0) {
+  return b64_tiled_launch(n, (tiles + kEncTilesPerGroup - 1) / kEncTilesPerGroup, [&](dim3 grid, uint32_t c0) {
     hipLaunchKernelGGL(b64_encode_kernel, grid, dim3(kB64Threads), 0, stream, data, data_off, size, text, text_off, tiles,
                        c0);
   });
