@@ -690,6 +690,7 @@ struct Source {
   uint64_t base_len = 0;
   std::vector<int> fds;           // file source: one fd per file, -1 = could not be opened
   bool pinned = false;            // [base, base+base_len) lies in a lbf_host_register'ed range
+  bool autopinned = false;        // ... or in the span run_job pinned for this job (pin_on_the_fly)
   unsigned threads = copy_threads();  // staging copy threads
 
   bool from_files() const { return !fds.empty(); }
@@ -896,17 +897,19 @@ constexpr uint64_t kDirectMinRun = 1ull << 20;
 // three times on the staged route (the caller's write, the staging memcpy's
 // read and write, the DMA's read) and its rate moves with the box's memcpy; a
 // registered one crosses it once (§3).  On this ROCm, hipHostRegister of a
-// whole 4 GiB job costs about 0.1 ms (tools/autopin_probe.py), so by default
-// the job's address span is registered in one piece before its first copy and
-// unregistered after its last (measured against the staging memcpy on one box,
-// profiles/r05/autopin/: 64 MiB 14.2 against 13.0, 1 GiB 45.2 against 41.8,
-// 4 GiB 50.7 against 49.6 GiB/s).  LBF_AUTOPIN_MB=W instead pins windows of W
-// MiB from a helper thread, at most kAhead windows ahead of the copies, and
-// unpins each once the worker has moved past it and its last copy has landed
-// (an event recorded after that copy); that form measured slower at 4 GiB
-// (46.8) and stays an A/B knob.  A window HIP refuses to pin (pinned
-// elsewhere) stays on the staged route, and so does a batch whose copy HIP
-// refuses (see worker_run).
+// whole 4 GiB job costs about 0.1 ms (tools/autopin_probe.py), so run_job
+// registers the job's address span in one piece before any worker starts and
+// unregisters it after every worker has drained; the workers see a registered
+// source and take the direct route (measured against the staging memcpy on one
+// box, profiles/r05/autopin/: 64 MiB 14.2 against 13.0, 1 GiB 45.2 against
+// 41.8, 4 GiB 50.7 against 49.6 GiB/s).  One registration per JOB, not per
+// worker: the workers' index ranges meet inside a page unless the buffer is
+// page-aligned, and two registrations of one page are refused below (round 5
+// first pinned per worker, and with two workers one of them staged).  Pinning
+// windows ahead of the copies from a helper thread measured slower (46.8 GiB/s
+// at 4 GiB, same profile) and was dropped.  A span HIP refuses to register is
+// staged, and so is a batch whose copy HIP refuses (see worker_run).
+//
 // Spans being pinned on the fly by running jobs, process-wide: two contexts
 // hashing the same pageable buffer at once must not both register it (one's
 // unregister could drop pages the other is still copying from), so a span that
@@ -928,175 +931,65 @@ void release_autopin(uintptr_t lo) {
   g_autopin.erase(lo);
 }
 
+// The whole pages holding [lo, hi), registered for the life of the object (the
+// owner destroys it only once every copy from the span has landed).
 class AutoPin {
  public:
-  AutoPin(int device, uintptr_t lo, uintptr_t hi, uint64_t window) : device_(device) {
+  AutoPin(uintptr_t lo, uintptr_t hi) {
     const uintptr_t page = (uintptr_t)sysconf(_SC_PAGESIZE);
-    lo &= ~(page - 1);
+    lo_ = lo & ~(page - 1);
     hi = (hi + page - 1) & ~(page - 1);
-    window = window ? std::max<uint64_t>(page, window / page * page) : hi - lo;  // 0: the span in one piece
-    for (uintptr_t a = lo; a < hi; a += window) win_.push_back(Window{a, std::min<uintptr_t>(hi, a + window)});
-    reserved_ = lo < hi && reserve_autopin(lo, hi);
-    span_lo_ = lo;
-    if (!reserved_) {  // another job pins (part of) it, or the caller registered it: staged
-      for (Window& w : win_) w.state = kFailed;
-      win_.resize(std::min<size_t>(win_.size(), 1));
+    if (lo_ >= hi || !reserve_autopin(lo_, hi)) return;  // another job pins (part of) it, or the caller does: staged
+    reserved_ = true;
+    const hipError_t e = hipHostRegister(reinterpret_cast<void*>(lo_), hi - lo_, hipHostRegisterPortable);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();  // pinned elsewhere, or no memory: the job is staged
       return;
     }
-    if (win_.size() == 1) {  // the whole span at once, on this thread
-      Window& w = win_[0];
-      const hipError_t e = hipHostRegister(reinterpret_cast<void*>(w.lo), w.hi - w.lo, hipHostRegisterPortable);
-      if (e != hipSuccess) (void)hipGetLastError();  // pinned elsewhere, or no memory: the job is staged
-      w.state = e == hipSuccess ? kPinned : kFailed;
-      if (e == hipSuccess) pinned_bytes_ = w.hi - w.lo;
-      return;
+    pinned_ = true;
+  }
+  ~AutoPin() {
+    if (pinned_) {
+      (void)hipHostUnregister(reinterpret_cast<void*>(lo_));
+      (void)hipGetLastError();
     }
-    for (Window& w : win_)
-      if (hipEventCreateWithFlags(&w.ev, hipEventDisableTiming) != hipSuccess) {
-        (void)hipGetLastError();
-        w.ev = nullptr;
-      }
-    th_ = std::thread([this] { loop(); });
+    if (reserved_) release_autopin(lo_);
   }
-  ~AutoPin() { finish(); }
-  // true once every window holding [a, b) is pinned; waits for the helper to get there
-  bool covered(uintptr_t a, uintptr_t b) {
-    std::unique_lock<std::mutex> g(mu_);
-    const size_t k0 = index(a), k1 = index(b - 1);
-    if (k0 >= win_.size() || k1 >= win_.size()) return false;
-    cursor_ = std::max(cursor_, k1);  // the helper pins up to kAhead windows past this group
-    cv_.notify_all();
-    for (size_t k = k0; k <= k1; ++k) {
-      cv_.wait(g, [&] { return win_[k].state != kPending || stop_; });
-      if (win_[k].state != kPinned) return false;
-    }
-    return true;
-  }
-  // a group's copies from [a, b) were issued on `stream`: record each window's
-  // event behind them (the last recording is the one its unpin waits for)
-  bool used(uintptr_t a, uintptr_t b, hipStream_t stream) {
-    if (win_.size() == 1) return true;  // unpinned only after the drain
-    std::lock_guard<std::mutex> g(mu_);
-    for (size_t k = index(a); k <= index(b - 1) && k < win_.size(); ++k) {
-      if (!win_[k].ev || hipEventRecord(win_[k].ev, stream) != hipSuccess) {
-        (void)hipGetLastError();
-        return false;
-      }
-      win_[k].used = true;
-    }
-    return true;
-  }
-  // copies from these windows were refused: stage what lies in them from now on
-  // (they stay pinned until retired, so their unpin still follows their copies)
-  void give_up(uintptr_t a, uintptr_t b) {
-    std::lock_guard<std::mutex> g(mu_);
-    for (size_t k = index(a); k <= index(b - 1) && k < win_.size(); ++k)
-      if (win_[k].state == kPinned) win_[k].state = kGivenUp;
-  }
-  // the worker will not read below `a` again: windows that end there can go
-  void retire_before(uintptr_t a) {
-    std::lock_guard<std::mutex> g(mu_);
-    while (retired_ < win_.size() && win_[retired_].hi <= a) ++retired_;
-    cv_.notify_all();
-  }
-  // every stream drained: unpin whatever is left and stop the helper
-  void finish() {
-    if (win_.size() <= 1 && !th_.joinable()) {  // the one-piece form: every copy has landed (drained)
-      if (!win_.empty() && (win_[0].state == kPinned || win_[0].state == kGivenUp)) {
-        (void)hipHostUnregister(reinterpret_cast<void*>(win_[0].lo));
-        (void)hipGetLastError();
-        win_[0].state = kUnpinned;
-      }
-      if (reserved_) release_autopin(span_lo_);
-      reserved_ = false;
-      return;
-    }
-    if (!th_.joinable()) return;
-    {
-      std::lock_guard<std::mutex> g(mu_);
-      retired_ = win_.size();
-      stop_ = true;
-    }
-    cv_.notify_all();
-    th_.join();
-    for (Window& w : win_)
-      if (w.ev) (void)hipEventDestroy(w.ev);
-    if (reserved_) release_autopin(span_lo_);
-    reserved_ = false;
-  }
-  uint64_t pinned_bytes() const { return pinned_bytes_; }
-  // bytes from a to the end of its window: one H2D may not cross a registration
-  // (HIP refuses a copy whose source spans two: "invalid argument")
-  uint64_t room(uintptr_t a) {
-    std::lock_guard<std::mutex> g(mu_);
-    const size_t k = index(a);
-    return k < win_.size() ? win_[k].hi - a : 0;
-  }
+  AutoPin(const AutoPin&) = delete;
+  AutoPin& operator=(const AutoPin&) = delete;
+  bool pinned() const { return pinned_; }
 
  private:
-  static constexpr int kPending = 0, kPinned = 1, kFailed = 2, kUnpinned = 3, kGivenUp = 4;
-  static constexpr size_t kAhead = 4;
-  struct Window {
-    uintptr_t lo, hi;
-    int state = kPending;
-    hipEvent_t ev = nullptr;
-    bool used = false;
-  };
-  size_t index(uintptr_t a) const {
-    if (win_.empty() || a < win_[0].lo) return win_.size();
-    const uint64_t w = win_[0].hi - win_[0].lo;
-    return (size_t)((a - win_[0].lo) / w);
-  }
-  void loop() {
-    (void)hipSetDevice(device_);
-    size_t next = 0, unpinned = 0;  // windows pinned (or refused) so far; windows unpinned so far
-    std::unique_lock<std::mutex> g(mu_);
-    for (;;) {
-      // retired windows first: the worker does not read their pages again
-      while (unpinned < std::min(retired_, next)) {
-        Window& w = win_[unpinned++];
-        if (w.state != kPinned && w.state != kGivenUp) continue;
-        g.unlock();
-        if (w.used && w.ev) (void)hipEventSynchronize(w.ev);  // its last copy has landed
-        (void)hipHostUnregister(reinterpret_cast<void*>(w.lo));
-        (void)hipGetLastError();
-        g.lock();
-        w.state = kUnpinned;
-      }
-      if (stop_) {  // finish(): every window retired; none is pinned past this point
-        for (size_t k = next; k < win_.size(); ++k) win_[k].state = kFailed;
-        cv_.notify_all();
-        if (unpinned >= next) return;
-        continue;
-      }
-      if (next < win_.size() && next <= cursor_ + kAhead) {
-        Window& w = win_[next];
-        g.unlock();
-        const hipError_t e = hipHostRegister(reinterpret_cast<void*>(w.lo), w.hi - w.lo, hipHostRegisterPortable);
-        if (e != hipSuccess) (void)hipGetLastError();  // pinned elsewhere, or no memory: that window is staged
-        g.lock();
-        w.state = e == hipSuccess ? kPinned : kFailed;
-        if (e == hipSuccess) pinned_bytes_ += w.hi - w.lo;
-        ++next;
-        cv_.notify_all();
-        continue;
-      }
-      cv_.wait(g, [&] {
-        return stop_ || unpinned < std::min(retired_, next) || (next < win_.size() && next <= cursor_ + kAhead);
-      });
-    }
-  }
-  int device_;
-  bool reserved_ = false;
-  uintptr_t span_lo_ = 0;
-  std::vector<Window> win_;
-  std::mutex mu_;
-  std::condition_variable cv_;
-  size_t cursor_ = 0, retired_ = 0;
-  bool stop_ = false;
-  uint64_t pinned_bytes_ = 0;
-  std::thread th_;
+  uintptr_t lo_ = 0;
+  bool reserved_ = false, pinned_ = false;
 };
+
+// The registration run_job makes for a memory job of LBF_AUTOPIN_MIN_MB (64)
+// and more whose chunks fill at least half of their address span (a scattered
+// table is staged: registering a span mostly of other data pins pages no copy
+// reads), or null.  The bytes are the union of the chunks for a table in offset
+// order, their sum (capped at the span) otherwise.
+std::unique_ptr<AutoPin> pin_on_the_fly(const Job& job, uint64_t n) {
+  if (job.src.from_files() || job.src.pinned || env_long("LBF_AUTOPIN", 1) != 1) return nullptr;
+  uint64_t lo = UINT64_MAX, hi = 0, bytes = 0, run_end = 0;
+  bool sorted = true;
+  for (uint64_t k = 0; k < n; ++k) {
+    const uint64_t o = job.offsets[k], sz = job.sizes[k];
+    if (sz == 0) continue;
+    if (k && o < job.offsets[k - 1]) sorted = false;
+    lo = std::min(lo, o);
+    hi = std::max(hi, o + sz);
+    if (!sorted || o >= run_end) bytes += sz;
+    else if (o + sz > run_end) bytes += o + sz - run_end;
+    run_end = std::max(run_end, o + sz);
+  }
+  bytes = std::min(bytes, hi > lo ? hi - lo : 0);
+  if (hi <= lo || bytes < (env_u64("LBF_AUTOPIN_MIN_MB", 64) << 20) || 2 * bytes < hi - lo) return nullptr;
+  const uintptr_t b = reinterpret_cast<uintptr_t>(job.src.base);
+  std::unique_ptr<AutoPin> pin(new AutoPin(b + lo, b + hi));
+  if (!pin->pinned()) pin.reset();
+  return pin;
+}
 
 // Process descriptors [begin, end) on one worker.  They are staged in source
 // order: sorted by offset (a stable permutation, skipped when the table is
@@ -1131,7 +1024,6 @@ int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
       break;
     }
   uint64_t job_bytes = 0;  // the union of this worker's runs
-  uint64_t span_lo = UINT64_MAX, span_hi = 0;  // the address span they lie in (memory jobs)
   {
     // Staging sized to the bytes this worker stages (the union of its runs):
     // a quarter of them per slot once they exceed kSplitMin, so a mid-sized job
@@ -1145,8 +1037,6 @@ int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
       const uint64_t k = order(q), o = job.offsets[k], sz = job.sizes[k];
       if (sz == 0 || sz + 15 > w.slot_max) continue;
       largest = std::max(largest, sz);
-      span_lo = std::min(span_lo, o);
-      span_hi = std::max(span_hi, o + sz);
       if (open && job.file(k) == run_file && o <= run_end + kJoinGap) {
         if (o + sz > run_end) bytes += o + sz - run_end, run_end = o + sz;
       } else {
@@ -1178,20 +1068,6 @@ int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
   const uint64_t direct_max_mb = env_u64("LBF_DIRECT_MAX_MB", 0);
   const uint64_t direct_max = direct_max_mb ? direct_max_mb << 20 : UINT64_MAX;
   const bool direct_job = job.src.pinned && job_bytes <= direct_max;
-  // Pin a large pageable job on the fly (AutoPin above; LBF_AUTOPIN=0 turns it
-  // off): jobs of LBF_AUTOPIN_MIN_MB (64) and more whose runs fill at least half
-  // of their address span
-  std::unique_ptr<AutoPin> autopin;
-  if (!job.src.pinned && !job.src.from_files() && env_long("LBF_AUTOPIN", 1) == 1 && span_hi > span_lo &&
-      job_bytes >= (env_u64("LBF_AUTOPIN_MIN_MB", 64) << 20) && 2 * job_bytes >= span_hi - span_lo) {
-    const uintptr_t b = reinterpret_cast<uintptr_t>(job.src.base);
-    const uint64_t window = env_u64("LBF_AUTOPIN_MB", 0) << 20;  // 0: the whole span in one piece
-    try {
-      autopin.reset(new AutoPin(w.device, b + span_lo, b + span_hi, window));
-    } catch (const std::exception&) {
-      autopin.reset();  // no helper thread: the staged route, as without the knob
-    }
-  }
   int cur = 0, hcur = 0;
   int prev_direct = -1;  // device slot of the last direct-route batch
   uint64_t i = begin;
@@ -1263,13 +1139,6 @@ int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
       // A registered source skips the ring: each run is copied to the device
       // straight from the caller's pinned memory, then the header follows.
       bool direct = direct_job && !runs.empty() && cursor >= runs.size() * kDirectMinRun;
-      const uintptr_t g_lo = runs.empty() ? 0 : reinterpret_cast<uintptr_t>(job.src.base) + runs.front().src;
-      const uintptr_t g_hi = runs.empty() ? 0 : reinterpret_cast<uintptr_t>(job.src.base) + runs.back().src +
-                                                     runs.back().len;
-      if (autopin && !runs.empty()) {
-        autopin->retire_before(g_lo);  // runs come in address order: nothing below this group is read again
-        direct = cursor >= runs.size() * kDirectMinRun && autopin->covered(g_lo, g_hi);
-      }
       for (Run& r : runs) r.avail = 0;
       if (direct) {
         // A batch's copies start only once the previous direct batch's have
@@ -1286,26 +1155,20 @@ int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
         // GiB/s, profiles/r02/registered_trace/piece_sweep/); ordered, whole runs are as fast
         // or faster (50.6 against 49.6-49.8 GiB/s at 4 GiB, direct_ordered/).
         const uint64_t piece = env_u64("LBF_DIRECT_PIECE_MB", 0) << 20;
-        bool refused = false;  // an on-the-fly window HIP cannot copy from (see below)
+        bool refused = false;  // a copy HIP refuses from an on-the-fly registration (see below)
         for (Run& r : runs) {
           const uint64_t step = piece ? piece : r.len;
           for (uint64_t at = 0, len = 0; at < r.len && rc == LBF_OK && !refused; at += len) {
             len = std::min(step, r.len - at);
-            if (autopin)  // on-the-fly windows are separate registrations: one copy per window
-              len = std::min<uint64_t>(len, autopin->room(reinterpret_cast<uintptr_t>(job.src.base + r.src + at)));
-            if (len == 0) {
-              rc = fail(LBF_ERR_INVALID, "on-the-fly pinning: a run outside its windows");
-              break;
-            }
             const hipError_t e = hipMemcpyAsync(s.d_buf + w.hdr_cap + r.dst + at, job.src.base + r.src + at, len,
                                                 hipMemcpyHostToDevice, s.stream);
-            if (e == hipErrorInvalidValue && autopin) {
-              // HIP lets a window be registered over a range the caller had
+            if (e == hipErrorInvalidValue && job.src.autopinned) {
+              // HIP lets a span be registered over a range the caller had
               // pinned itself, then resolves copies in that range to the
               // caller's (smaller) registration and refuses them at enqueue.
-              // Such a window is given up and this batch staged; the copies
-              // already queued run before the staged ones on the same stream,
-              // which overwrite whatever they wrote.
+              // Such a batch is staged; the copies already queued run before
+              // the staged ones on the same stream, which overwrite whatever
+              // they wrote.
               (void)hipGetLastError();
               refused = true;
             } else if (!hip_ok(e, "hipMemcpyAsync(H2D, registered source)")) {
@@ -1317,15 +1180,10 @@ int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
         }
         if (rc) break;
         if (refused) {
-          autopin->give_up(g_lo, g_hi);
           direct = false;
           for (Run& r : runs) r.avail = 0;
         } else {
           if (!hip_ok(hipEventRecord(s.copied, s.stream), "hipEventRecord")) break;
-          if (autopin && !autopin->used(g_lo, g_hi, s.stream)) {
-            rc = fail(LBF_ERR_HIP, "hipEventRecord (on-the-fly pinning)");
-            break;
-          }
           prev_direct = cur;
         }
       }
@@ -1430,7 +1288,6 @@ int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
     s.pending = false;
   }
   for (HostSlot& h : w.host) h.in_flight = false;
-  if (autopin) autopin->finish();  // every copy has landed (drained above): unpin the rest
   trim_dev_slots(w);
   return rc;
 }
@@ -1457,6 +1314,10 @@ int run_job(lbf_ctx* ctx, Job job, uint64_t n) {
   std::lock_guard<std::mutex> lock(ctx->mu);
   KeepCurrentDevice keep;  // worker 0 (and any inline worker) runs on this thread
   if (!job.src.from_files()) job.src.pinned = in_registered(ctx, job.src.base, job.src.base_len);
+  // Declared before the workers run and destroyed after they return: every
+  // worker drains its streams before returning, so no copy outlives the span.
+  const std::unique_ptr<AutoPin> autopin = pin_on_the_fly(job, n);
+  if (autopin) job.src.pinned = job.src.autopinned = true;
   const size_t nw = ctx->workers.size();
   if (nw == 1 || n < 2 * nw) return worker_run(ctx->workers[0], job, 0, n);
   std::vector<int> rcs(nw, LBF_OK);

@@ -50,23 +50,21 @@ def test_registered_contiguous_hash_and_verify(workers, oracle, monkeypatch):
         exp[flips, 19] ^= 1
         v = h.verify_chunks(buf, offs, sizes, exp)
         assert np.flatnonzero(~v).tolist() == flips
-        # unregistered: pinned on the fly for the job (the default since round 5)
-        # when a worker's share reaches LBF_AUTOPIN_MIN_MB (64 MiB: one worker's
-        # 96 MiB does, two workers' 48 MiB each do not), so the same groups go
-        # direct; with LBF_AUTOPIN=0 through staging; same digests either way
+        # unregistered: pinned on the fly for the job (the default since round 5,
+        # jobs of LBF_AUTOPIN_MIN_MB = 64 MiB and more), once for the whole job
+        # whatever the number of workers (two workers' halves meet inside a page
+        # unless the buffer is page-aligned), so the same groups go direct;
+        # under the threshold, or with LBF_AUTOPIN=0, through staging
         h.unregister_host(buf)
         s1 = h.staging_stats()
         assert np.array_equal(h.hash_chunks(buf, offs, sizes), want)
         d = _delta(h, s1)
-        if workers == 1:
-            assert d["direct"] == buf.size - 12345 and d["staged"] == 12345, d
-        else:
-            assert d["direct"] == 0 and d["staged"] == buf.size, d
-        monkeypatch.setenv("LBF_AUTOPIN_MIN_MB", "32")
+        assert d["direct"] == buf.size - 12345 and d["staged"] == 12345, d
+        monkeypatch.setenv("LBF_AUTOPIN_MIN_MB", "128")
         s1 = h.staging_stats()
         assert np.array_equal(h.hash_chunks(buf, offs, sizes), want)
         d = _delta(h, s1)
-        assert d["direct"] == buf.size - 12345 and d["staged"] == 12345, d
+        assert d["direct"] == 0 and d["staged"] == buf.size, d
         monkeypatch.delenv("LBF_AUTOPIN_MIN_MB")
         monkeypatch.setenv("LBF_AUTOPIN", "0")
         s1 = h.staging_stats()
@@ -262,17 +260,17 @@ def test_buffer_the_caller_pinned_whole_goes_direct(oracle, hasher, size):
         assert hip.hipHostUnregister(ctypes.c_void_p(base)) == 0
 
 
-@pytest.mark.parametrize("window_mb", [0, 64])
+@pytest.mark.parametrize("workers", [1, 3])
 @pytest.mark.parametrize("mib,piece_pinned", [(600, False), (600, True)])
-def test_on_the_fly_pinning(oracle, hasher, monkeypatch, mib, piece_pinned, window_mb):
+def test_on_the_fly_pinning(oracle, monkeypatch, mib, piece_pinned, workers):
     """A large pageable job is pinned on the fly: its whole
-    span in one registration (the default, window 0) or window by window from a
-    helper thread (LBF_AUTOPIN_MB, an A/B knob).  It goes the direct route and
-    leaves nothing pinned behind; a span or window HIP cannot copy from (part of
-    it pinned elsewhere) is staged.  Digests equal the oracle's either way."""
+    span in one registration made before the workers start, whatever their
+    number.  It goes the direct route and leaves nothing pinned behind; a batch
+    HIP cannot copy from (part of it pinned elsewhere) is staged.  Digests equal
+    the oracle's either way."""
     import ctypes
     hip = _hip()
-    monkeypatch.setenv("LBF_AUTOPIN_MB", str(window_mb))
+    hasher = _ctx(monkeypatch, LBF_WORKERS_PER_DEVICE=workers)
     buf = oracle.synth(95, 0, mib * MIB + 4321, nthreads=8)
     offs, sizes = chunk_table(buf.size, 256 * 1024)
     want = oracle.sha1_batch(buf, offs, sizes, nthreads=8)
@@ -286,11 +284,14 @@ def test_on_the_fly_pinning(oracle, hasher, monkeypatch, mib, piece_pinned, wind
         assert np.array_equal(hasher.hash_chunks(buf, offs, sizes), want)
         d = _delta(hasher, s0)
         assert d["direct"] + d["staged"] >= buf.size
-        if piece_pinned:
-            assert d["staged"] > 0
-        if not piece_pinned or window_mb:
-            assert d["direct"] > buf.size // 2, d
+        if piece_pinned and workers == 1:
+            # HIP refuses a copy that starts inside the foreign registration and
+            # runs past its end; one worker's batches have one starting there
+            # (three workers' do not, and go direct throughout, as measured)
+            assert d["staged"] > 0, d
+        assert d["direct"] > buf.size // 2, d
     finally:
+        hasher.close()
         if other:
             assert hip.hipHostUnregister(ctypes.c_void_p(other)) == 0
     # nothing of the job is left pinned: the caller can pin it all itself

@@ -10,8 +10,7 @@
 //   lbf_verify_encode_b64_batch + lbf_b64_verify_batch (the wire form both ways:
 //   text slots at ragged offsets, some texts cut short; no byte between slots
 //   written, a short decode's slot tail zeroed)
-// with large pageable jobs pinned on the fly in a third of the contexts, in
-// windows in another third (LBF_AUTOPIN*),
+// with pageable jobs pinned on the fly in half of the contexts (LBF_AUTOPIN*),
 // against the oracle (oracle/sha1_oracle.c, compiled in as the checker).  Half
 // the jobs read from memory registered with the context, and half the
 // contexts then take three concurrent callers with 24-40 MiB batches (enough
@@ -72,12 +71,9 @@ int main(int argc, char** argv) {
     setenv("LBF_SLOT_MB", std::to_string(slot_mb).c_str(), 1);
     setenv("LBF_TEST_FAULT_GROUP", fault ? std::to_string(uni(0, 3)).c_str() : "-1", 1);
     setenv("LBF_TEST_FAULT_WORKER", std::to_string(uni(0, workers - 1)).c_str(), 1);
-    // on-the-fly pinning of pageable jobs (read per job): off, the whole span, or
-    // 1-2 MiB windows pinned by a helper thread, from 1 MiB of job on
-    const int autopin = (int)uni(0, 2);
-    setenv("LBF_AUTOPIN", autopin ? "1" : "0", 1);
+    // on-the-fly pinning of pageable jobs (read per job): off or on, from 1 MiB of job on
+    setenv("LBF_AUTOPIN", uni(0, 1) ? "1" : "0", 1);
     setenv("LBF_AUTOPIN_MIN_MB", "1", 1);
-    setenv("LBF_AUTOPIN_MB", autopin == 2 ? std::to_string(uni(1, 2)).c_str() : "0", 1);
     lbf_ctx* ctx = nullptr;
     if (lbf_ctx_create(1, &ctx) != LBF_OK) {
       std::fprintf(stderr, "lbf_ctx_create: %s\n", lbf_last_error());

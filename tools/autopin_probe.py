@@ -12,8 +12,6 @@ all in one process and lease, best of 3 after a warm pass:
                 pinned memory; registration and hashing timed together
   autopin       the library's own on-the-fly pinning (lbf_capi.cpp AutoPin; the
                 default since round 5): the job's span registered in one piece
-  autopin_windows  the same with LBF_AUTOPIN_MB=--piece-mib: a helper thread pins
-                windows ahead of the copies and unpins them behind
   registered    the buffer registered outside the timing (what a caller that
                 reuses its buffer gets: the ceiling of the pinned routes)
 plus the cost of pinning and unpinning alone (GiB/s of hipHostRegister /
@@ -117,9 +115,6 @@ def main():
             assert bytes(g[-1]) == want_last
             r["autopin"] = best_of(3, lambda: h.hash_chunks(data, offs, sizes_))
             autopin_direct = (h.staging_stats()["direct"] - s0["direct"]) / (4 * data.size)
-            os.environ["LBF_AUTOPIN_MB"] = str(a.piece_mib)  # windows pinned ahead by a helper thread
-            r["autopin_windows"] = best_of(3, lambda: h.hash_chunks(data, offs, sizes_))
-            os.environ["LBF_AUTOPIN_MB"] = "0"
             os.environ["LBF_AUTOPIN"] = "0"
             r["staged_again"] = best_of(3, lambda: h.hash_chunks(data, offs, sizes_))
 
