@@ -623,7 +623,11 @@ def inproc_leg(buf, slice_bytes, cs, shard_starts, slice_hashes):
         info = [h.worker_info(w) for w in range(h.num_workers)]
         ndev = h.num_devices
         h.hash_chunks(big, offs, sizes)  # warm: every worker's staging and device slots
+        s0 = h.staging_stats()
         pag, d_pag = best(h, 2)
+        # the pageable passes' route: pinned on the fly for the whole job (one
+        # registration shared by every worker) unless LBF_AUTOPIN=0
+        pag_direct = (h.staging_stats()["direct"] - s0["direct"]) / (2 * total)
         t0 = time.perf_counter()
         h.register_host(big)
         reg_s = time.perf_counter() - t0
@@ -640,6 +644,7 @@ def inproc_leg(buf, slice_bytes, cs, shard_starts, slice_hashes):
         "devices": ndev, "workers": len(info), "workers_per_device": int(os.environ.get("LBF_WORKERS_PER_DEVICE", "1")),
         "bytes": total, "chunk_size": cs,
         "registered_gibs": round(reg, 3), "register_s": round(reg_s, 4), "pageable_gibs": round(pag, 3),
+        "pageable_direct_fraction": round(pag_direct, 4),
         "direct_bytes": st["direct"],
         "parity_per_slice": ok, "parity": all(ok) and bool(np.array_equal(d_reg, d_pag)),
         "placement": info,

@@ -133,6 +133,7 @@ def _check_line(out, n):
     assert out["e2e"]["parity"] is True and out["e2e"]["parity_per_rank"] == [1] * n
     assert "error" not in out["e2e_inprocess"], out["e2e_inprocess"]
     assert out["e2e_inprocess"]["parity"] is True and out["e2e_inprocess"]["parity_per_slice"] == [1] * n
+    assert 0 <= out["e2e_inprocess"]["pageable_direct_fraction"] <= 1
 
 
 @pytest.mark.parametrize("n", [2, 8])
