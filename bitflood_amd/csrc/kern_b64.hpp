@@ -88,28 +88,38 @@ __device__ __forceinline__ uint32_t wg_exclusive_scan(uint32_t v, uint32_t* sums
 // ---------------------------------------------------------------------------
 // Tiles of whole lines.  The encoder's text is lines of 18 groups: 72 alphabet
 // characters and a separator (base64.h:197-205's '\n', framed as a space), 73
-// characters that decode to 54 bytes.  A tile of 64 lines is 4,672 characters
-// and 3,456 bytes, both multiples of 16, so tile k of a chunk reads text
-// [4672k, +4672) and writes bytes [3456k, +3456) (or the reverse for the
-// encode) with 16-byte accesses whenever the chunk's slot is 16-byte aligned,
-// and no group or separator crosses a tile.  grid.x = chunks x tiles; every
-// workgroup stages its tile's input span in LDS with coalesced 16-byte loads
-// (global_load_dwordx4 + ds_write_b128), then each lane builds one 16-byte
-// block of the output from LDS and stores it: one pass over HBM in each
-// direction, nothing re-read.  (Round 4's kernels read bytes straight from HBM,
+// characters that decode to 54 bytes.  A tile of L lines is 73L characters
+// and 54L bytes, so tile k of a chunk reads text [73Lk, +73L) and writes bytes
+// [54Lk, +54L) (or the reverse for the encode), and no group or separator
+// crosses a tile; where the tile's output is whole 16-byte blocks it is
+// written with 16-byte stores whenever the chunk's slot is 16-byte aligned.
+// grid = (groups of tiles, chunks); every workgroup stages its tile's input
+// span in LDS with coalesced 16-byte loads (global_load_dwordx4 +
+// ds_write_b128), then each lane builds one or two 16-byte blocks of the output
+// from LDS and stores them: one pass over HBM in each direction, nothing
+// re-read.  (Round 4's kernels read bytes straight from HBM,
 // 16 byte loads per four groups per lane, and spent 74-86 % of their wave
 // cycles waiting on memory at 0.23-0.30 of the HBM peak)
 // ---------------------------------------------------------------------------
-constexpr uint32_t kB64TileLines = 64;
-constexpr uint32_t kB64TileText = kB64TileLines * 73;    // 4,672 characters
-constexpr uint32_t kB64TileBytes = kB64TileLines * 54;   // 3,456 bytes
-constexpr uint32_t kB64TileGroups = kB64TileLines * 18;  // 1,152 groups
+// The encode's tile: 112 lines, 6,048 bytes -> 8,176 characters = 511 output
+// blocks, two per lane (64 lines made 292 blocks: a second pass for 36 lanes).
+// 120.5-121.0 us per 1,024 x 256 KiB against 136.1-137.4 for 64 lines, alternating on one box
+// (profiles/r05/b64_geometry/ab_traces_enc_tiles.json).  Both texts and bytes of
+// a tile must be whole 16-byte blocks: a multiple of 16 lines.
+#ifndef LBF_B64_ENC_LINES
+#define LBF_B64_ENC_LINES 112
+#endif
+constexpr uint32_t kB64TileLines = LBF_B64_ENC_LINES;
+constexpr uint32_t kB64TileText = kB64TileLines * 73;    // 8,176 characters
+constexpr uint32_t kB64TileBytes = kB64TileLines * 54;   // 6,048 bytes
+constexpr uint32_t kB64TileGroups = kB64TileLines * 18;  // 2,016 groups
 static_assert(kB64TileText % 16 == 0 && kB64TileBytes % 16 == 0, "tiles of 16-byte blocks");
 // The decode's tile (its output, the bytes, must be whole 16-byte blocks: a
 // multiple of 8 lines; its text tile is read at any phase): 72 lines, 5,256
 // characters -> 3,888 bytes, 243 of the 256 lanes busy (64 lines: 216).  That
 // and eight tiles per workgroup measured 157.6 us per 1,024 x 256 KiB against
-// 171.5-171.8 for 64 lines and four (tools/b64_ab_trace.sh, profiles/r05/b64/).
+// 171.5-171.8 for 64 lines and four (tools/b64_ab_trace.sh, profiles/r05/b64/);
+// 144 lines (two blocks per lane) measured 175-179 us.
 // LBF_B64_DEC_LINES, LBF_B64_DEC_TILES_PER_GROUP and LBF_B64_ENC_TILES_PER_GROUP
 // exist for A/B builds (tools/b64_ab_build.sh).
 #ifndef LBF_B64_DEC_LINES
@@ -117,33 +127,34 @@ static_assert(kB64TileText % 16 == 0 && kB64TileBytes % 16 == 0, "tiles of 16-by
 #endif
 constexpr uint32_t kDecLines = LBF_B64_DEC_LINES;
 constexpr uint32_t kDecText = kDecLines * 73, kDecBytes = kDecLines * 54, kDecGroups = kDecLines * 18;
-static_assert(kDecBytes % 16 == 0 && kDecBytes / 16 <= 256, "a decode tile is at most one 16-byte block per lane");
+static_assert(kDecBytes % 16 == 0, "a decode tile is whole 16-byte blocks of output");
 typedef uint32_t b64_u32x4 __attribute__((ext_vector_type(4)));  // what the nontemporal builtins take
 
 // Stage global bytes [src, src + len) in LDS as the aligned 16-byte blocks that
 // hold them: afterwards lds byte (delta + k) = src[k], delta = src mod 16.  The
 // blocks are read whole (a 16-byte block holding one byte of the span lies in
-// the same page, so this never reads an unmapped address).  Up to two blocks
-// per lane.  load() issues both of a lane's loads and returns at once; store()
+// the same page, so this never reads an unmapped address).  Up to kPer blocks
+// per lane.  load() issues all of a lane's loads and returns at once; store()
 // waits for them and writes LDS, so work placed between the two (the decode
 // table, the last group's check) runs while the loads are in flight.
+template <uint32_t kPer>
 struct B64Stage {
-  b64_u32x4 v0, v1;
+  b64_u32x4 v[kPer];
   uint32_t blocks = 0, delta = 0;
   __device__ __forceinline__ void load(const uint8_t* src, uint32_t len) {
     const uintptr_t a = reinterpret_cast<uintptr_t>(src);
     delta = (uint32_t)(a & 15u);
     const b64_u32x4* g = reinterpret_cast<const b64_u32x4*>(a - delta);
     blocks = (delta + len + 15) / 16;
-    const uint32_t k0 = threadIdx.x, k1 = threadIdx.x + kB64Threads;
-    if (k0 < blocks) v0 = __builtin_nontemporal_load(g + k0);
-    if (k1 < blocks) v1 = __builtin_nontemporal_load(g + k1);
+#pragma unroll
+    for (uint32_t k = 0; k < kPer; ++k)
+      if (threadIdx.x + k * kB64Threads < blocks) v[k] = __builtin_nontemporal_load(g + threadIdx.x + k * kB64Threads);
   }
   __device__ __forceinline__ void store(uint4* lds) const {
     b64_u32x4* l = reinterpret_cast<b64_u32x4*>(lds);
-    const uint32_t k0 = threadIdx.x, k1 = threadIdx.x + kB64Threads;
-    if (k0 < blocks) l[k0] = v0;
-    if (k1 < blocks) l[k1] = v1;
+#pragma unroll
+    for (uint32_t k = 0; k < kPer; ++k)
+      if (threadIdx.x + k * kB64Threads < blocks) l[threadIdx.x + k * kB64Threads] = v[k];
   }
 };
 
@@ -199,13 +210,15 @@ __device__ __forceinline__ bool b64_canon_groups(uint32_t len, uint32_t* groups)
   return true;
 }
 
-// One tile of the one-pass decode from its text in LDS (sb, from byte
-// `delta`): lane u < 216 builds and stores bytes [16u, 16u + 16) of the tile.
-// Returns true when the lane saw a character that breaks the layout.
-__device__ __forceinline__ bool b64_decode_tile(const uint8_t* sb, uint32_t delta, const uint8_t* tab, uint32_t tile,
-                                                uint32_t groups, uint32_t len, uint64_t want, uint32_t limit,
-                                                uint8_t* o) {
-  if (threadIdx.x >= kDecBytes / 16) return false;
+// One block of a tile of the one-pass decode from its text in LDS (sb, from
+// byte `delta`): in pass p, lane v builds and stores bytes [16u, 16u + 16) of
+// the tile, u = v + 256p (if the tile has that block).  Returns true when the
+// lane saw a character that breaks the layout.
+template <uint32_t kPass>
+__device__ __forceinline__ bool b64_decode_block(const uint8_t* sb, uint32_t delta, const uint8_t* tab, uint32_t tile,
+                                                 uint32_t groups, uint32_t len, uint64_t want, uint32_t limit,
+                                                 uint8_t* o) {
+  if (threadIdx.x + kPass * kB64Threads >= kDecBytes / 16) return false;
   // Bytes [16u, 16u + 16) of the tile come from its groups g0 .. g0 + 5, whose
   // characters lie in [c0, c0 + 25): 24 characters and at most one separator,
   // after group 17 - r0 of the window when r0 >= 12.  One window of eight
@@ -213,7 +226,7 @@ __device__ __forceinline__ bool b64_decode_tile(const uint8_t* sb, uint32_t delt
   // with v_alignbyte (no divergent branch: groups past the chunk's end are
   // decoded from whatever lies there and masked below).
   const uint32_t* w = reinterpret_cast<const uint32_t*>(sb);
-  const uint32_t b0 = 16 * threadIdx.x, g0 = b0 / 3, phase = b0 - 3 * g0;
+  const uint32_t b0 = 16 * (threadIdx.x + kPass * kB64Threads), g0 = b0 / 3, phase = b0 - 3 * g0;
   const uint32_t l0 = g0 / 18, r0 = g0 - 18 * l0;
   const uint32_t c0 = delta + 4 * g0 + l0, sh0 = c0 & 3u;
   const uint32_t* wb = w + (c0 >> 2);
@@ -268,6 +281,20 @@ __device__ __forceinline__ bool b64_decode_tile(const uint8_t* sb, uint32_t delt
   return bad;
 }
 
+// A tile: every lane its block of each pass (one pass for the shipped 243-block
+// tile; the block index is written out in each pass rather than passed in, which
+// kept the shipped kernel at 71 VGPRs where a block-index argument made it 87).
+__device__ __forceinline__ bool b64_decode_tile(const uint8_t* sb, uint32_t delta, const uint8_t* tab, uint32_t tile,
+                                                uint32_t groups, uint32_t len, uint64_t want, uint32_t limit,
+                                                uint8_t* o) {
+  static_assert(kDecBytes / 16 <= 3 * kB64Threads, "three blocks per lane at most");
+  bool bad = b64_decode_block<0>(sb, delta, tab, tile, groups, len, want, limit, o);
+  if constexpr (kDecBytes / 16 > kB64Threads) bad |= b64_decode_block<1>(sb, delta, tab, tile, groups, len, want, limit, o);
+  if constexpr (kDecBytes / 16 > 2 * kB64Threads)
+    bad |= b64_decode_block<2>(sb, delta, tab, tile, groups, len, want, limit, o);
+  return bad;
+}
+
 // Tiles per workgroup: a workgroup takes kDecTilesPerGroup (kEncTilesPerGroup) consecutive tiles
 // of its chunk and double-buffers them in LDS, so the next tile's loads are in
 // flight while it decodes (or encodes) the current one: one barrier per tile,
@@ -276,7 +303,7 @@ __device__ __forceinline__ bool b64_decode_tile(const uint8_t* sb, uint32_t delt
 #define LBF_B64_DEC_TILES_PER_GROUP 8
 #endif
 #ifndef LBF_B64_ENC_TILES_PER_GROUP
-#define LBF_B64_ENC_TILES_PER_GROUP 4  // eight measured 5 % slower for the encode
+#define LBF_B64_ENC_TILES_PER_GROUP 2  // of 112 lines (1 and 3: 0.5-1 % slower; 64-line tiles: 4, eight 5 % slower)
 #endif
 constexpr uint32_t kDecTilesPerGroup = LBF_B64_DEC_TILES_PER_GROUP, kEncTilesPerGroup = LBF_B64_ENC_TILES_PER_GROUP;
 
@@ -298,7 +325,7 @@ __global__ void __launch_bounds__(kB64Threads) b64_decode_canon_kernel(const uin
                                                                        uint32_t chunk0) {
   // a tile's span, its phase, and slack for the last lane's 32-byte window read
   constexpr uint32_t kStage = (kDecText + 15 + 15) / 16 + 2;
-  static_assert(kStage <= 2 * kB64Threads, "two blocks per lane at most");
+  constexpr uint32_t kPer = (kStage + kB64Threads - 1) / kB64Threads;  // staged blocks per lane
   __shared__ uint4 stage[2][kStage];
   __shared__ uint8_t tab[256];
   __shared__ uint32_t last_shared;
@@ -317,7 +344,7 @@ __global__ void __launch_bounds__(kB64Threads) b64_decode_canon_kernel(const uin
   const uint32_t t1 = min(own, t0 + kDecTilesPerGroup);
   const uint8_t* t = text + text_off[i];
   uint8_t* o = out + out_off[i];
-  B64Stage st;
+  B64Stage<kPer> st;
   auto load = [&](uint32_t tile) {
     const uint32_t tbeg = tile * kDecText;
     st.blocks = 0;
@@ -571,7 +598,7 @@ __global__ void __launch_bounds__(kB64Threads) b64_encode_kernel(const uint8_t* 
   // a tile's span, its phase, and slack for the group reads of the last window
   // (computed for every word, used only inside the tile)
   constexpr uint32_t kStage = (kB64TileBytes + 15) / 16 + 4;
-  static_assert(kStage <= 2 * kB64Threads, "two blocks per lane at most");
+  constexpr uint32_t kPer = (kStage + kB64Threads - 1) / kB64Threads;  // staged blocks per lane
   __shared__ uint4 stage[2][kStage];
   __shared__ uint8_t alpha[64];
   const uint32_t i = chunk0 + blockIdx.y, t0 = blockIdx.x * kEncTilesPerGroup;
@@ -582,7 +609,7 @@ __global__ void __launch_bounds__(kB64Threads) b64_encode_kernel(const uint8_t* 
   const uint32_t t1 = min(own, t0 + kEncTilesPerGroup);
   const uint8_t* d = data + data_off[i];
   uint8_t* t = text + text_off[i];
-  B64Stage st;
+  B64Stage<kPer> st;
   auto load = [&](uint32_t tile) {
     const uint32_t dbeg = tile * kB64TileBytes;
     st.blocks = 0;

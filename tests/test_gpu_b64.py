@@ -256,14 +256,17 @@ def test_outputs_touch_nothing_outside_their_slots(hasher):
 
 def _encoder_layout_sizes():
     """Chunk sizes whose text exercises every length form of the encoder's
-    layout and the one-pass kernels' tiles (64 lines = 3,456 bytes = 4,672
-    characters): no tail, one or two tail bytes, a padded last group that is
-    the 18th of its line (length 73q + 72: 52, 53, 106, 107, ...), a text that
-    ends with a separator (54k bytes), tile edges, a C5 chunk."""
+    layout and the one-pass kernels' tiles (encode 112 lines = 6,048 bytes =
+    8,176 characters, decode 72 lines = 3,888 bytes = 5,256 characters; 64
+    lines = 3,456 bytes, round 5's first tile): no tail, one or two tail
+    bytes, a padded last group that is the 18th of its line (length 73q + 72:
+    52, 53, 106, 107, ...), a text that ends with a separator (54k bytes), tile
+    edges, a C5 chunk."""
     s = {0, 1, 2, 3, 51, 52, 53, 54, 55, 105, 106, 107, 108, 161, 162}
-    for k in (1, 2, 3, 76):
-        for d in (-3, -2, -1, 0, 1, 2, 3):
-            s.add(3456 * k + d)
+    for tile, ks in ((3456, (1, 2, 3, 76)), (6048, (1, 2, 43)), (3888, (1, 2, 67))):
+        for k in ks:
+            for d in (-3, -2, -1, 0, 1, 2, 3):
+                s.add(tile * k + d)
     for g in (17, 35, 18 * 64 - 1, 18 * 64 + 17, 18 * 200 + 17):  # full groups = 18q + 17
         s.update({3 * g + 1, 3 * g + 2})
     s.update({65536, 262144, 262145, 262146})
