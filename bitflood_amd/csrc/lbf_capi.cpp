@@ -968,7 +968,9 @@ class AutoPin {
 // and more whose chunks fill at least half of their address span (a scattered
 // table is staged: registering a span mostly of other data pins pages no copy
 // reads), or null.  The bytes are the union of the chunks for a table in offset
-// order, their sum (capped at the span) otherwise.
+// order, their sum (capped at the span) otherwise.  A span larger than half of
+// the host's physical memory is staged too: pinning it would lock most of RAM
+// for the length of the call.
 std::unique_ptr<AutoPin> pin_on_the_fly(const Job& job, uint64_t n) {
   if (job.src.from_files() || job.src.pinned || env_long("LBF_AUTOPIN", 1) != 1) return nullptr;
   uint64_t lo = UINT64_MAX, hi = 0, bytes = 0, run_end = 0;
@@ -985,6 +987,8 @@ std::unique_ptr<AutoPin> pin_on_the_fly(const Job& job, uint64_t n) {
   }
   bytes = std::min(bytes, hi > lo ? hi - lo : 0);
   if (hi <= lo || bytes < (env_u64("LBF_AUTOPIN_MIN_MB", 64) << 20) || 2 * bytes < hi - lo) return nullptr;
+  const long pages = sysconf(_SC_PHYS_PAGES), page = sysconf(_SC_PAGESIZE);
+  if (pages > 0 && page > 0 && hi - lo > (uint64_t)pages * (uint64_t)page / 2) return nullptr;
   const uintptr_t b = reinterpret_cast<uintptr_t>(job.src.base);
   std::unique_ptr<AutoPin> pin(new AutoPin(b + lo, b + hi));
   if (!pin->pinned()) pin.reset();
