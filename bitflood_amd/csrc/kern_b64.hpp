@@ -119,7 +119,9 @@ static_assert(kB64TileText % 16 == 0 && kB64TileBytes % 16 == 0, "tiles of 16-by
 // characters -> 3,888 bytes, 243 of the 256 lanes busy (64 lines: 216).  That
 // and eight tiles per workgroup measured 157.6 us per 1,024 x 256 KiB against
 // 171.5-171.8 for 64 lines and four (tools/b64_ab_trace.sh, profiles/r05/b64/);
-// 144 lines (two blocks per lane) measured 175-179 us.
+// 144 lines (two blocks per lane) measured 175-179 us.  The leaner block below
+// (62 VGPRs, 8 waves per SIMD) then runs best at four tiles per workgroup:
+// 129.7-130.7 us (profiles/r05/b64_geometry/ab_traces_dec_v2.json).
 // LBF_B64_DEC_LINES, LBF_B64_DEC_TILES_PER_GROUP and LBF_B64_ENC_TILES_PER_GROUP
 // exist for A/B builds (tools/b64_ab_build.sh).
 #ifndef LBF_B64_DEC_LINES
@@ -213,7 +215,11 @@ __device__ __forceinline__ bool b64_canon_groups(uint32_t len, uint32_t* groups)
 // One block of a tile of the one-pass decode from its text in LDS (sb, from
 // byte `delta`): in pass p, lane v builds and stores bytes [16u, 16u + 16) of
 // the tile, u = v + 256p (if the tile has that block).  Returns true when the
-// lane saw a character that breaks the layout.
+// lane saw a character that breaks the layout.  The kernel is VALU-bound
+// (about 70 % of its time was VALU issue at 230 instructions per block), so the
+// block keeps its instruction count down: the layout checks fold into two flag
+// words, the sextets are joined unmasked, and the 18 bytes are packed with five
+// v_perm_b32 (157 -> 133 us per 1,024 x 256 KiB).
 template <uint32_t kPass>
 __device__ __forceinline__ bool b64_decode_block(const uint8_t* sb, uint32_t delta, const uint8_t* tab, uint32_t tile,
                                                  uint32_t groups, uint32_t len, uint64_t want, uint32_t limit,
@@ -236,6 +242,10 @@ __device__ __forceinline__ bool b64_decode_block(const uint8_t* sb, uint32_t del
   const uint32_t gbase = tile * kDecGroups + g0;  // the chunk's index of group g0
   bool bad = false;
   uint32_t x[6];
+  // Table entries are 0..63, '=' 64 and anything else 255, so (entry >> 6)
+  // is 0 exactly for an alphabet character: two flag bits per group, at 2j,
+  // for all four characters (finner) and the first two (fhead).
+  uint32_t finner = 0, fhead = 0;
 #pragma unroll
   for (int j = 0; j < 6; ++j) {
     const uint32_t sep = r0 + j >= 18 ? 1u : 0u;
@@ -243,12 +253,24 @@ __device__ __forceinline__ bool b64_decode_block(const uint8_t* sb, uint32_t del
     const uint32_t lo = off >= 4 ? win[j + 1] : win[j], hi = off >= 4 ? win[j + 2] : win[j + 1];
     const uint32_t c = __builtin_amdgcn_alignbyte(hi, lo, off & 3u);
     const uint32_t s0 = tab[c & 255], s1 = tab[(c >> 8) & 255], s2 = tab[(c >> 16) & 255], s3 = tab[c >> 24];
-    const uint32_t gg = gbase + j;
-    // inside the text every character is in the alphabet; the last group's
-    // padding is checked by the kernel
-    const bool inner = ((s0 | s1 | s2 | s3) & ~63u) != 0, head = ((s0 | s1) & ~63u) != 0;
-    bad |= (gg + 1 < groups && inner) || (gg + 1 == groups && head);
-    x[j] = ((s0 & 63) << 18) | ((s1 & 63) << 12) | ((s2 & 63) << 6) | (s3 & 63);
+    const uint32_t o2 = s0 | s1, o4 = o2 | s2 | s3;
+    finner |= (o4 >> 6) << (2 * j);
+    fhead |= (o2 >> 6) << (2 * j);
+    // unmasked: an entry above 63 spoils only its own group's bytes, and such a
+    // group is either marked bad or the last group's '=' padding, whose bytes
+    // (those a '=' in character 2 or 3 reaches) lie past the decoded length
+    // and are zeroed below
+    x[j] = (((s0 << 6) | s1) << 12) | ((s2 << 6) | s3);
+  }
+  {
+    // window groups j < rel lie inside the text (all four characters in the
+    // alphabet); group rel is the chunk's last (its first two in the alphabet;
+    // the kernel checks its padding)
+    const int32_t rel = (int32_t)groups - 1 - (int32_t)gbase;
+    const uint32_t nin = (uint32_t)min(max(rel, 0), 6);
+    const uint32_t inner_mask = (1u << (2 * nin)) - 1u;
+    const uint32_t head_mask = rel >= 0 && rel < 6 ? 3u << (2 * rel) : 0u;
+    bad |= ((finner & inner_mask) | (fhead & head_mask)) != 0;
   }
   // the separator after group 17 - r0 (when in the window): any character outside the alphabet
   {
@@ -259,12 +281,13 @@ __device__ __forceinline__ bool b64_decode_block(const uint8_t* sb, uint32_t del
     bad |= check && tab[sb[at]] != kB64Skip;
   }
   // the 18 bytes of the six groups, as little-endian words
-  auto by = [&](int j, int k) { return (x[j] >> (16 - 8 * k)) & 255u; };
-  const uint32_t W0 = by(0, 0) | by(0, 1) << 8 | by(0, 2) << 16 | by(1, 0) << 24;
-  const uint32_t W1 = by(1, 1) | by(1, 2) << 8 | by(2, 0) << 16 | by(2, 1) << 24;
-  const uint32_t W2 = by(2, 2) | by(3, 0) << 8 | by(3, 1) << 16 | by(3, 2) << 24;
-  const uint32_t W3 = by(4, 0) | by(4, 1) << 8 | by(4, 2) << 16 | by(5, 0) << 24;
-  const uint32_t W4 = by(5, 1) | by(5, 2) << 8;
+  // group j's bytes are x[j]'s bytes 2, 1, 0: one v_perm_b32 per word (selector
+  // bytes 0-3 pick from the second source, 4-7 from the first, 12 gives 0)
+  const uint32_t W0 = __builtin_amdgcn_perm(x[1], x[0], 0x06000102u);
+  const uint32_t W1 = __builtin_amdgcn_perm(x[2], x[1], 0x05060001u);
+  const uint32_t W2 = __builtin_amdgcn_perm(x[3], x[2], 0x04050600u);
+  const uint32_t W3 = __builtin_amdgcn_perm(x[5], x[4], 0x06000102u);
+  const uint32_t W4 = __builtin_amdgcn_perm(x[5], x[5], 0x0C0C0001u);
   uint4 v = make_uint4(__builtin_amdgcn_alignbyte(W1, W0, phase), __builtin_amdgcn_alignbyte(W2, W1, phase),
                        __builtin_amdgcn_alignbyte(W3, W2, phase), __builtin_amdgcn_alignbyte(W4, W3, phase));
   const uint64_t pos = (uint64_t)tile * kDecBytes + b0;
@@ -300,7 +323,7 @@ __device__ __forceinline__ bool b64_decode_tile(const uint8_t* sb, uint32_t delt
 // flight while it decodes (or encodes) the current one: one barrier per tile,
 // and a CU's resident workgroups keep loads outstanding through their compute.
 #ifndef LBF_B64_DEC_TILES_PER_GROUP
-#define LBF_B64_DEC_TILES_PER_GROUP 8
+#define LBF_B64_DEC_TILES_PER_GROUP 4  // 2, 3, 6, 8: 141, 134, 140, 133 us against 130 (256 KiB chunks: 68 tiles)
 #endif
 #ifndef LBF_B64_ENC_TILES_PER_GROUP
 #define LBF_B64_ENC_TILES_PER_GROUP 2  // of 112 lines (1 and 3: 0.5-1 % slower; 64-line tiles: 4, eight 5 % slower)
