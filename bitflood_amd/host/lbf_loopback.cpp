@@ -737,7 +737,7 @@ int main(int argc, char** argv) {
   if (o.gpu_encode && !o.synthetic) die("--gpu-encode needs --synthetic (the file seeder reads and verifies in one call)");
   if (o.role != Opts::BOTH && o.dir.empty()) die("--role seeder/leecher needs --dir (the directory both peers share)");
   if (o.role == Opts::LEECHER && (o.port <= 0 || o.port > 65535)) die("--role leecher needs --port");
-  if (o.port > 65535) die("--port must be 0..65535");
+  if (o.port < 0 || o.port > 65535) die("--port must be 0..65535");
   if (o.dir.empty()) {
     const char* t = getenv("TMPDIR");
     char tmpl[512];

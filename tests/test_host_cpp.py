@@ -168,7 +168,8 @@ def test_loopback_role_options_checked_before_the_gpu(tmp_path):
     for args, msg in [(["--role", "leecher", "--dir", str(tmp_path)], "needs --port"),
                       (["--role", "seeder"], "needs --dir"),
                       (["--role", "peer"], "--role takes"),
-                      (["--role", "seeder", "--dir", str(tmp_path), "--port", "70000"], "--port must be")]:
+                      (["--role", "seeder", "--dir", str(tmp_path), "--port", "70000"], "--port must be"),
+                      (["--role", "seeder", "--dir", str(tmp_path), "--port", "-1"], "--port must be")]:
         out = subprocess.run([lb] + args, capture_output=True, text=True, timeout=60)
         assert out.returncode == 2 and msg in out.stderr, (args, out.stderr)
 
