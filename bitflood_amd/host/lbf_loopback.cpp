@@ -717,7 +717,11 @@ int main(int argc, char** argv) {
       else if (r == "seeder") o.role = Opts::SEEDER;
       else if (r == "leecher") o.role = Opts::LEECHER;
       else die("--role takes both, seeder or leecher");
-    } else if (a == "--port") o.port = (int)strtol(val(), nullptr, 10);
+    } else if (a == "--port") {
+      const long v = strtol(val(), nullptr, 10);
+      if (v < 0 || v > 65535) die("--port must be 0..65535");
+      o.port = (int)v;
+    }
     else if (a == "--port-file") o.port_file = val();
     else {
       fprintf(stderr,
@@ -737,7 +741,6 @@ int main(int argc, char** argv) {
   if (o.gpu_encode && !o.synthetic) die("--gpu-encode needs --synthetic (the file seeder reads and verifies in one call)");
   if (o.role != Opts::BOTH && o.dir.empty()) die("--role seeder/leecher needs --dir (the directory both peers share)");
   if (o.role == Opts::LEECHER && (o.port <= 0 || o.port > 65535)) die("--role leecher needs --port");
-  if (o.port < 0 || o.port > 65535) die("--port must be 0..65535");
   if (o.dir.empty()) {
     const char* t = getenv("TMPDIR");
     char tmpl[512];
