@@ -291,19 +291,28 @@ def barrier(world):
         dist.barrier()
 
 
+DIGEST_ERRORS = {}  # kernel -> why its digest could not be read (traffic_null_reason)
+
+
 def kernel_code_digest(kernel, lib_path=None):
-    """(mangled symbol, sha256 of its gfx950 machine code) of `kernel` (e.g.
-    'sha1_pc4_kernel<true, 2, 8>') in the library this process loaded
-    (bitflood_amd/kernel_digest.py reads the code object out of the .so), or
-    (None, None) when it cannot be found."""
+    """(mangled symbol, sha256 of its gfx950 machine code and descriptor) of
+    `kernel` (e.g. 'sha1_pc4_kernel<true, 2, 8>') in the library this process
+    loaded (bitflood_amd/kernel_digest.py reads the code object out of the
+    .so), or (None, None) when it cannot be found; the reason is kept in
+    DIGEST_ERRORS[kernel]."""
     from bitflood_amd import _capi
     from bitflood_amd import kernel_digest as KD
     try:
         d = KD.kernel_digests(lib_path or _capi.LIB_PATH)
         sym = KD.symbol_for(d, kernel)
-        return (sym, d[sym]) if sym and d.get(sym) else (None, None)
-    except (OSError, ValueError, IndexError, struct.error):
-        return None, None
+        if sym and d.get(sym):
+            return sym, d[sym]
+        DIGEST_ERRORS[kernel] = f"{kernel} not found (or ambiguous) in the loaded library's gfx950 code objects"
+    except KD.CompressedBundle as e:
+        DIGEST_ERRORS[kernel] = f"compressed bundle: {e}"
+    except (OSError, ValueError, IndexError, struct.error) as e:
+        DIGEST_ERRORS[kernel] = f"{type(e).__name__}: {e}"
+    return None, None
 
 
 def traffic_from_profiles(file_bytes, chunk_size, kernel, code_sha=None, path=None):
@@ -332,6 +341,8 @@ def traffic_from_profiles(file_bytes, chunk_size, kernel, code_sha=None, path=No
             continue
         if code_sha is None:
             reason = f"the loaded library's code for {kernel} could not be read"
+            if DIGEST_ERRORS.get(kernel):
+                reason += f" ({DIGEST_ERRORS[kernel]})"
             continue
         if rec != code_sha:
             reason = (f"the loaded library's {kernel} is not the code that was profiled ({e.get('source')}: "
@@ -682,6 +693,20 @@ def check_golden(gold, digests):
     return 1 if ok else 0
 
 
+def config_entry(name, length, cs, ms, ok, gold, kernel, pmc_path=None):
+    """One other_configs record: rate, HBM fraction and, through the same rule
+    as the main line (traffic_from_profiles), the PMC traffic recorded for
+    this kernel's machine code at this size, or null with the reason."""
+    code_sym, code_sha = kernel_code_digest(kernel)
+    traffic, src, why = traffic_from_profiles(length, cs, kernel, code_sha, path=pmc_path)
+    return {"workload": name, "bytes": length, "chunk_size": cs, "chunks": length // cs, "kernel": kernel,
+            "ms_per_launch": round(ms, 4), "gibs": round(length / GIB / (ms / 1e3), 1),
+            "hbm_frac": round(length / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+            "traffic": traffic, "traffic_ratio": round(traffic / length, 5) if traffic else None,
+            "traffic_source": src, "traffic_null_reason": why,
+            "kernel_code_sha256": code_sha, "kernel_symbol": code_sym, "golden": gold, "parity": ok}
+
+
 def other_configs():
     """C3 and C4 (BASELINE.json configs[2], configs[3] per GPU), device-resident,
     measured after the main line at N=1 and checked against their goldens:
@@ -704,10 +729,7 @@ def other_configs():
         return e0.elapsed_time(e1) / reps
 
     def entry(name, length, cs, ms, ok, gold):
-        return {"workload": name, "bytes": length, "chunk_size": cs, "chunks": length // cs,
-                "kernel": KERNELS.get(H.load().lbf_kernel_for(length // cs), "?"), "ms_per_launch": round(ms, 4),
-                "gibs": round(length / GIB / (ms / 1e3), 1),
-                "hbm_frac": round(length / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4), "golden": gold, "parity": ok}
+        return config_entry(name, length, cs, ms, ok, gold, KERNELS.get(H.load().lbf_kernel_for(length // cs), "?"))
 
     for name in ("C3", "C4"):
         buf = dig = None

@@ -127,6 +127,9 @@ static_assert(kB64TileText % 16 == 0 && kB64TileBytes % 16 == 0, "tiles of 16-by
 #ifndef LBF_B64_DEC_LINES
 #define LBF_B64_DEC_LINES 72
 #endif
+#ifndef LBF_B64_DEC_WIN64
+#define LBF_B64_DEC_WIN64 0
+#endif
 constexpr uint32_t kDecLines = LBF_B64_DEC_LINES;
 constexpr uint32_t kDecText = kDecLines * 73, kDecBytes = kDecLines * 54, kDecGroups = kDecLines * 18;
 static_assert(kDecBytes % 16 == 0, "a decode tile is whole 16-byte blocks of output");
@@ -235,10 +238,25 @@ __device__ __forceinline__ bool b64_decode_block(const uint8_t* sb, uint32_t del
   const uint32_t b0 = 16 * (threadIdx.x + kPass * kB64Threads), g0 = b0 / 3, phase = b0 - 3 * g0;
   const uint32_t l0 = g0 / 18, r0 = g0 - 18 * l0;
   const uint32_t c0 = delta + 4 * g0 + l0, sh0 = c0 & 3u;
+#if LBF_B64_DEC_WIN64
+  // A/B: the window as five 8-byte reads from the even dword below it.  Lanes'
+  // windows start ~5.3 dwords apart, so eight ds_read_b32 (banks (a/4) mod 32,
+  // 32-lane groups) meet ~3-way bank conflicts; ds_read_b64 banks mod 64.
+  const uint32_t r = (c0 >> 2) & 1u;
+  const uint2* wb = reinterpret_cast<const uint2*>(w + ((c0 >> 2) & ~1u));
+  uint32_t win[10];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    const uint2 x2 = wb[k];
+    win[2 * k] = x2.x;
+    win[2 * k + 1] = x2.y;
+  }
+#else
   const uint32_t* wb = w + (c0 >> 2);
   uint32_t win[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) win[k] = wb[k];
+#endif
   const uint32_t gbase = tile * kDecGroups + g0;  // the chunk's index of group g0
   bool bad = false;
   uint32_t x[6];
@@ -250,7 +268,13 @@ __device__ __forceinline__ bool b64_decode_block(const uint8_t* sb, uint32_t del
   for (int j = 0; j < 6; ++j) {
     const uint32_t sep = r0 + j >= 18 ? 1u : 0u;
     const uint32_t off = sh0 + sep;  // 0..4: this group's offset from dword j of the window
+#if LBF_B64_DEC_WIN64
+    const uint32_t q = r + (off >> 2);  // 0..2 dwords past win[j]
+    const uint32_t lo = q == 0 ? win[j] : q == 1 ? win[j + 1] : win[j + 2];
+    const uint32_t hi = q == 0 ? win[j + 1] : q == 1 ? win[j + 2] : win[j + 3];
+#else
     const uint32_t lo = off >= 4 ? win[j + 1] : win[j], hi = off >= 4 ? win[j + 2] : win[j + 1];
+#endif
     const uint32_t c = __builtin_amdgcn_alignbyte(hi, lo, off & 3u);
     const uint32_t s0 = tab[c & 255], s1 = tab[(c >> 8) & 255], s2 = tab[(c >> 16) & 255], s3 = tab[c >> 24];
     const uint32_t o2 = s0 | s1, o4 = o2 | s2 | s3;

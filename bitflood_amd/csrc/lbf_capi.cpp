@@ -27,6 +27,7 @@
 #include <condition_variable>
 #include <cerrno>
 #include <cstdio>
+#include <chrono>
 #include <cstdlib>
 #include <functional>
 #include <iterator>
@@ -360,6 +361,7 @@ struct DevSlot {
   hipStream_t stream = nullptr;
   uint8_t* d_buf = nullptr;  // header | data (hdr_cap + slot_bytes)
   uint8_t* h_hdr = nullptr;  // pinned header of a multi-piece batch (hdr_cap)
+  uint8_t* h_edge = nullptr;  // pinned bounce for a direct batch's bytes outside the pinned pages (edge_cap())
   uint8_t* d_out = nullptr;  // desc_cap * 20: digests, or verdicts
   uint8_t* h_out = nullptr;  // pinned
   std::vector<uint8_t> ok;   // 1 = chunk bytes fully available
@@ -480,6 +482,7 @@ namespace {
 // pinned; `owned` = this context registered it (and unregisters it).
 struct Registered {
   uintptr_t user = 0;  // the pointer the caller passed (the unregister key)
+  uintptr_t user_end = 0;  // user + the length the caller passed
   uintptr_t lo = 0, hi = 0;
   bool owned = false;
 };
@@ -527,11 +530,18 @@ void host_free(void* p) {
   (void)hipHostFree(p);  // release paths: a failure has nowhere to go
 }
 
+// An on-the-fly registration pins only the pages that lie wholly inside the
+// job's bytes (pin_on_the_fly), so a direct batch may hold up to a page at
+// each end of the job that is not pinned: those bytes are bounced through
+// this much pinned memory per device slot.
+uint64_t edge_cap() { return 2 * (uint64_t)sysconf(_SC_PAGESIZE); }
+
 int dev_slot_init(Worker& w, DevSlot& d) {
   LBF_HIP_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
   LBF_HIP_TRY(hipMalloc((void**)&d.d_out, w.desc_cap * 20));
   LBF_HIP_TRY(host_alloc(w, (void**)&d.h_out, w.desc_cap * 20));
   LBF_HIP_TRY(host_alloc(w, (void**)&d.h_hdr, w.hdr_cap));
+  LBF_HIP_TRY(host_alloc(w, (void**)&d.h_edge, edge_cap()));
   if (w.slot_bytes) LBF_HIP_TRY(hipMalloc((void**)&d.d_buf, w.hdr_cap + w.slot_bytes));
   LBF_HIP_TRY(hipEventCreateWithFlags(&d.copied, hipEventDisableTiming));
   d.ok.assign(w.desc_cap, 0);
@@ -545,6 +555,7 @@ void dev_slot_free(DevSlot& d) {
   if (d.d_out) (void)hipFree(d.d_out);
   host_free(d.h_out);
   host_free(d.h_hdr);
+  host_free(d.h_edge);
   if (d.copied) (void)hipEventDestroy(d.copied);
   if (d.stream) (void)hipStreamDestroy(d.stream);
   d = DevSlot{};
@@ -691,6 +702,10 @@ struct Source {
   std::vector<int> fds;           // file source: one fd per file, -1 = could not be opened
   bool pinned = false;            // [base, base+base_len) lies in a lbf_host_register'ed range
   bool autopinned = false;        // ... or in the span run_job pinned for this job (pin_on_the_fly)
+  // The pinned addresses of a pinned source, [pin_lo, pin_hi): all of it for
+  // a registered one; for an on-the-fly one the pages wholly inside the job's
+  // bytes, so up to a page at either end lies outside (bounced, worker_run).
+  uintptr_t pin_lo = 0, pin_hi = 0;
   unsigned threads = copy_threads();  // staging copy threads
 
   bool from_files() const { return !fds.empty(); }
@@ -910,38 +925,54 @@ constexpr uint64_t kDirectMinRun = 1ull << 20;
 // at 4 GiB, same profile) and was dropped.  A span HIP refuses to register is
 // staged, and so is a batch whose copy HIP refuses (see worker_run).
 //
-// Spans being pinned on the fly by running jobs, process-wide: two contexts
-// hashing the same pageable buffer at once must not both register it (one's
-// unregister could drop pages the other is still copying from), so a span that
-// overlaps another job's, or a range pinned through lbf_host_register, is staged.
+// The pages pinned on the fly by running jobs, process-wide, [lo, hi) each.
+// Two contexts hashing the same pageable buffer at once must not both register
+// it (one's unregister could drop pages the other is still copying from), so a
+// span that overlaps another job's, or a range pinned through
+// lbf_host_register, is staged.  The other direction matters as much (ADVICE
+// r05): lbf_host_register must never take a job's pages for "pinned by
+// someone else" and adopt them, since the job unpins them when it ends; it
+// waits on g_autopin_cv until no running job's pages overlap its range.  Lock
+// order: a context's mu, then g_autopin_mu, then g_pin_mu.
 bool pin_table_overlaps(uintptr_t lo, uintptr_t hi);  // lbf_host_register's table (below)
 std::mutex g_autopin_mu;
+std::condition_variable g_autopin_cv;       // notified when a span is released
 std::map<uintptr_t, uintptr_t> g_autopin;  // lo -> hi of the spans reserved now
+bool autopin_overlaps_locked(uintptr_t lo, uintptr_t hi) {
+  auto next = g_autopin.lower_bound(lo);
+  return (next != g_autopin.end() && next->first < hi) || (next != g_autopin.begin() && std::prev(next)->second > lo);
+}
 bool reserve_autopin(uintptr_t lo, uintptr_t hi) {
   std::lock_guard<std::mutex> g(g_autopin_mu);
-  auto next = g_autopin.lower_bound(lo);
-  if ((next != g_autopin.end() && next->first < hi) || (next != g_autopin.begin() && std::prev(next)->second > lo))
-    return false;
-  if (pin_table_overlaps(lo, hi)) return false;
+  if (autopin_overlaps_locked(lo, hi) || pin_table_overlaps(lo, hi)) return false;
   g_autopin[lo] = hi;
   return true;
 }
 void release_autopin(uintptr_t lo) {
-  std::lock_guard<std::mutex> g(g_autopin_mu);
-  g_autopin.erase(lo);
+  {
+    std::lock_guard<std::mutex> g(g_autopin_mu);
+    g_autopin.erase(lo);
+  }
+  g_autopin_cv.notify_all();
 }
 
-// The whole pages holding [lo, hi), registered for the life of the object (the
-// owner destroys it only once every copy from the span has landed).
+// The pages wholly inside the job's bytes [lo, hi), registered for the life of
+// the object (the owner destroys it only once every copy from them has
+// landed).  Rounding inward, not outward, is what keeps the library off memory
+// it was not handed: the first and last page of a span
+// that does not start and end on a page boundary also hold the caller's other
+// data, which the caller may pin itself while the job runs (an outward span
+// made that hipHostRegister fail), so they stay pageable and a direct batch
+// bounces the few bytes of the job that lie on them (worker_run).
 class AutoPin {
  public:
   AutoPin(uintptr_t lo, uintptr_t hi) {
     const uintptr_t page = (uintptr_t)sysconf(_SC_PAGESIZE);
-    lo_ = lo & ~(page - 1);
-    hi = (hi + page - 1) & ~(page - 1);
-    if (lo_ >= hi || !reserve_autopin(lo_, hi)) return;  // another job pins (part of) it, or the caller does: staged
+    lo_ = (lo + page - 1) & ~(page - 1);
+    hi_ = hi & ~(page - 1);
+    if (lo_ >= hi_ || !reserve_autopin(lo_, hi_)) return;  // another job pins (part of) it, or the caller does: staged
     reserved_ = true;
-    const hipError_t e = hipHostRegister(reinterpret_cast<void*>(lo_), hi - lo_, hipHostRegisterPortable);
+    const hipError_t e = hipHostRegister(reinterpret_cast<void*>(lo_), hi_ - lo_, hipHostRegisterPortable);
     if (e != hipSuccess) {
       (void)hipGetLastError();  // pinned elsewhere, or no memory: the job is staged
       return;
@@ -958,22 +989,26 @@ class AutoPin {
   AutoPin(const AutoPin&) = delete;
   AutoPin& operator=(const AutoPin&) = delete;
   bool pinned() const { return pinned_; }
+  uintptr_t lo() const { return lo_; }
+  uintptr_t hi() const { return hi_; }
 
  private:
-  uintptr_t lo_ = 0;
+  uintptr_t lo_ = 0, hi_ = 0;
   bool reserved_ = false, pinned_ = false;
 };
 
 // The registration run_job makes for a memory job of LBF_AUTOPIN_MIN_MB (64)
-// and more whose chunks fill at least half of their address span (a scattered
-// table is staged: registering a span mostly of other data pins pages no copy
-// reads), or null.  The bytes are the union of the chunks for a table in offset
-// order, their sum (capped at the span) otherwise.  A span larger than half of
-// the host's physical memory is staged too: pinning it would lock most of RAM
-// for the length of the call.
+// and more whose chunks cover their address span without a gap, or null.  The
+// union of the chunks is measured in offset order (a sorted copy of the table
+// when it is not sorted already, so repeated chunks count once: ADVICE r05).
+// A table with gaps is staged: pinning across a gap pins pages no copy reads,
+// bytes the caller did not hand over (round 5 pinned any span its chunks
+// filled half of).  A span larger than half of the host's physical memory is
+// staged too: pinning it would lock most of RAM for the length of the call.
 std::unique_ptr<AutoPin> pin_on_the_fly(const Job& job, uint64_t n) {
   if (job.src.from_files() || job.src.pinned || env_long("LBF_AUTOPIN", 1) != 1) return nullptr;
-  uint64_t lo = UINT64_MAX, hi = 0, bytes = 0, run_end = 0;
+  const uint64_t min_bytes = env_u64("LBF_AUTOPIN_MIN_MB", 64) << 20;
+  uint64_t lo = UINT64_MAX, hi = 0, sum = 0;
   bool sorted = true;
   for (uint64_t k = 0; k < n; ++k) {
     const uint64_t o = job.offsets[k], sz = job.sizes[k];
@@ -981,14 +1016,25 @@ std::unique_ptr<AutoPin> pin_on_the_fly(const Job& job, uint64_t n) {
     if (k && o < job.offsets[k - 1]) sorted = false;
     lo = std::min(lo, o);
     hi = std::max(hi, o + sz);
-    if (!sorted || o >= run_end) bytes += sz;
-    else if (o + sz > run_end) bytes += o + sz - run_end;
-    run_end = std::max(run_end, o + sz);
+    sum += sz;
   }
-  bytes = std::min(bytes, hi > lo ? hi - lo : 0);
-  if (hi <= lo || bytes < (env_u64("LBF_AUTOPIN_MIN_MB", 64) << 20) || 2 * bytes < hi - lo) return nullptr;
+  // the union is at most the sum and at most the span: both must reach the bar
+  if (hi <= lo || hi - lo < min_bytes || sum < hi - lo) return nullptr;
   const long pages = sysconf(_SC_PHYS_PAGES), page = sysconf(_SC_PAGESIZE);
   if (pages > 0 && page > 0 && hi - lo > (uint64_t)pages * (uint64_t)page / 2) return nullptr;
+  std::vector<uint64_t> perm;
+  if (!sorted) {
+    perm.resize(n);
+    for (uint64_t k = 0; k < n; ++k) perm[k] = k;
+    std::sort(perm.begin(), perm.end(), [&](uint64_t x, uint64_t y) { return job.offsets[x] < job.offsets[y]; });
+  }
+  uint64_t run_end = lo;
+  for (uint64_t q = 0; q < n; ++q) {
+    const uint64_t k = sorted ? q : perm[q], o = job.offsets[k], sz = job.sizes[k];
+    if (sz == 0) continue;
+    if (o > run_end) return nullptr;  // a gap
+    run_end = std::max(run_end, o + sz);
+  }
   const uintptr_t b = reinterpret_cast<uintptr_t>(job.src.base);
   std::unique_ptr<AutoPin> pin(new AutoPin(b + lo, b + hi));
   if (!pin->pinned()) pin.reset();
@@ -1143,6 +1189,7 @@ int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
       // A registered source skips the ring: each run is copied to the device
       // straight from the caller's pinned memory, then the header follows.
       bool direct = direct_job && !runs.empty() && cursor >= runs.size() * kDirectMinRun;
+      uint64_t edge_bytes = 0;
       for (Run& r : runs) r.avail = 0;
       if (direct) {
         // A batch's copies start only once the previous direct batch's have
@@ -1160,28 +1207,53 @@ int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
         // or faster (50.6 against 49.6-49.8 GiB/s at 4 GiB, direct_ordered/).
         const uint64_t piece = env_u64("LBF_DIRECT_PIECE_MB", 0) << 20;
         bool refused = false;  // a copy HIP refuses from an on-the-fly registration (see below)
-        for (Run& r : runs) {
-          const uint64_t step = piece ? piece : r.len;
-          for (uint64_t at = 0, len = 0; at < r.len && rc == LBF_OK && !refused; at += len) {
-            len = std::min(step, r.len - at);
-            const hipError_t e = hipMemcpyAsync(s.d_buf + w.hdr_cap + r.dst + at, job.src.base + r.src + at, len,
-                                                hipMemcpyHostToDevice, s.stream);
-            if (e == hipErrorInvalidValue && job.src.autopinned) {
-              // HIP lets a span be registered over a range the caller had
-              // pinned itself, then resolves copies in that range to the
-              // caller's (smaller) registration and refuses them at enqueue.
-              // Such a batch is staged; the copies already queued run before
-              // the staged ones on the same stream, which overwrite whatever
-              // they wrote.
-              (void)hipGetLastError();
+        // A run's bytes outside the pinned pages (an on-the-fly span's first
+        // and last partial page, AutoPin) go through the slot's pinned bounce:
+        // the slot's stream is idle here, so its previous contents are spent.
+        // Bytes that do not fit it send the batch through staging.
+        const uint64_t pin_lo = job.src.pin_lo - reinterpret_cast<uintptr_t>(job.src.base);
+        const uint64_t pin_hi = job.src.pin_hi - reinterpret_cast<uintptr_t>(job.src.base);
+        uint64_t bounced = 0;
+        auto copy = [&](uint64_t dst, uint64_t src, uint64_t len) {  // one H2D of source bytes [src, src + len)
+          const uint8_t* from = job.src.base + src;
+          if (src < pin_lo || src + len > pin_hi) {
+            if (bounced + len > edge_cap()) {
               refused = true;
-            } else if (!hip_ok(e, "hipMemcpyAsync(H2D, registered source)")) {
-              break;
+              return;
             }
+            memcpy(s.h_edge + bounced, from, len);
+            from = s.h_edge + bounced;
+            bounced += len;
           }
+          const hipError_t e = hipMemcpyAsync(s.d_buf + w.hdr_cap + dst, from, len, hipMemcpyHostToDevice, s.stream);
+          if (e == hipErrorInvalidValue && job.src.autopinned) {
+            // HIP lets a span be registered over a range the caller had
+            // pinned itself, then resolves copies in that range to the
+            // caller's (smaller) registration and refuses them at enqueue.
+            // Such a batch is staged; the copies already queued run before
+            // the staged ones on the same stream, which overwrite whatever
+            // they wrote.
+            (void)hipGetLastError();
+            refused = true;
+          } else {
+            hip_ok(e, "hipMemcpyAsync(H2D, registered source)");
+          }
+        };
+        for (Run& r : runs) {
+          // [r.src, r.src + r.len) cut at the pinned pages' ends: head, body, tail
+          const uint64_t end = r.src + r.len;
+          const uint64_t b0 = std::min(std::max(r.src, pin_lo), end), b1 = std::max(std::min(end, pin_hi), b0);
+          if (b0 > r.src) copy(r.dst, r.src, b0 - r.src);
+          const uint64_t step = piece ? piece : b1 - b0;
+          for (uint64_t at = b0, len = 0; at < b1 && rc == LBF_OK && !refused; at += len) {
+            len = std::min(step, b1 - at);
+            copy(r.dst + (at - r.src), at, len);
+          }
+          if (end > b1 && rc == LBF_OK && !refused) copy(r.dst + (b1 - r.src), b1, end - b1);
           if (rc || refused) break;
           r.avail = r.len;
         }
+        edge_bytes = refused ? 0 : bounced;
         if (rc) break;
         if (refused) {
           direct = false;
@@ -1194,7 +1266,9 @@ int worker_run(Worker& w, const Job& job, uint64_t begin, uint64_t end) {
       const bool single = !direct && hdr + cursor <= w.pin_bytes;
       const uint64_t data_off = single ? hdr : w.hdr_cap;
       uint8_t* h_header = nullptr;
-      (direct ? w.bytes_direct : w.bytes_staged) += cursor;
+      // (a direct batch's bounced edge bytes count as staged: they took a host copy)
+      (direct ? w.bytes_direct : w.bytes_staged) += cursor - edge_bytes;
+      w.bytes_staged += edge_bytes;
       std::vector<bool> cut_short(runs.size(), false);
       size_t first_run = 0;
       for (uint64_t pstart = 0; !direct && (pstart < cursor || (single && pstart == 0)) && rc == LBF_OK;) {
@@ -1307,21 +1381,36 @@ int validate_memory_job(const Job& job, uint64_t n) {
 
 // Contiguous index ranges per worker, one host thread each (bound to its
 // worker's NUMA node), no collective.
+// A memory source lies in a registered range: the pages this library pinned,
+// or, for memory pinned by someone else, the caller's own bytes (only those
+// were shown to lie in one pinned allocation, lbf_host_register).
 bool in_registered(const lbf_ctx* ctx, const uint8_t* base, uint64_t len) {
   const uintptr_t a = reinterpret_cast<uintptr_t>(base);
-  for (const Registered& r : ctx->regs)
-    if (a >= r.lo && a <= r.hi && len <= r.hi - a) return true;
+  for (const Registered& r : ctx->regs) {
+    const uintptr_t lo = r.owned ? r.lo : r.user, hi = r.owned ? r.hi : r.user_end;
+    if (a >= lo && a <= hi && len <= hi - a) return true;
+  }
   return false;
 }
 
 int run_job(lbf_ctx* ctx, Job job, uint64_t n) {
   std::lock_guard<std::mutex> lock(ctx->mu);
   KeepCurrentDevice keep;  // worker 0 (and any inline worker) runs on this thread
-  if (!job.src.from_files()) job.src.pinned = in_registered(ctx, job.src.base, job.src.base_len);
+  if (!job.src.from_files() && in_registered(ctx, job.src.base, job.src.base_len)) {
+    job.src.pinned = true;
+    job.src.pin_lo = reinterpret_cast<uintptr_t>(job.src.base);
+    job.src.pin_hi = job.src.pin_lo + job.src.base_len;
+  }
   // Declared before the workers run and destroyed after they return: every
   // worker drains its streams before returning, so no copy outlives the span.
   const std::unique_ptr<AutoPin> autopin = pin_on_the_fly(job, n);
-  if (autopin) job.src.pinned = job.src.autopinned = true;
+  if (autopin) {
+    job.src.pinned = job.src.autopinned = true;
+    job.src.pin_lo = autopin->lo();
+    job.src.pin_hi = autopin->hi();
+  }
+  if (const uint64_t hold = env_u64("LBF_TEST_AUTOPIN_HOLD_MS", 0); hold && autopin)
+    std::this_thread::sleep_for(std::chrono::milliseconds(hold));  // tests only: keep the span pinned a while
   const size_t nw = ctx->workers.size();
   if (nw == 1 || n < 2 * nw) return worker_run(ctx->workers[0], job, 0, n);
   std::vector<int> rcs(nw, LBF_OK);
@@ -1558,6 +1647,7 @@ extern "C" int lbf_host_register(lbf_ctx* ctx, const void* ptr, uint64_t len) {
   if (len > UINTPTR_MAX - a - page) return fail(LBF_ERR_INVALID, "lbf_host_register: range wraps");
   Registered r;
   r.user = a;
+  r.user_end = a + len;
   r.lo = a & ~(page - 1);
   r.hi = (a + len + page - 1) & ~(page - 1);
   return guarded([&] {
@@ -1568,6 +1658,14 @@ extern "C" int lbf_host_register(lbf_ctx* ctx, const void* ptr, uint64_t len) {
                     "lbf_host_register: range shares pages with one this context already holds (pinning is per "
                     "page: give each registered buffer pages of its own)");
     ctx->regs.reserve(ctx->regs.size() + 1);  // nothing below may throw once pinned
+    // Pages a running job pinned on the fly are that job's: it unpins them
+    // when it ends.  Taken below for "pinned by someone else", they would
+    // leave this registration pointing at pageable memory and its batches
+    // copying "directly" from it.  So wait for every such job to
+    // end; holding g_autopin_mu from here on keeps a new job from pinning the
+    // range before it is in g_pins (reserve_autopin checks that table).
+    std::unique_lock<std::mutex> spans(g_autopin_mu);
+    g_autopin_cv.wait(spans, [&] { return !autopin_overlaps_locked(r.lo, r.hi); });
     std::lock_guard<std::mutex> pins(g_pin_mu);
     auto next = g_pins.lower_bound(r.lo);
     if (next != g_pins.end() && next->first == r.lo && next->second.hi == r.hi) {
@@ -1839,6 +1937,14 @@ int slot_runs(const uint64_t* off, const uint64_t* len, uint64_t n, const char* 
 }
 }  // namespace
 
+// The wire kernels keep text and byte positions inside a chunk, and their
+// tile counts, in 32 bits (kern_b64.hpp): (len + tile - 1) / tile and
+// tile * tile_text must not wrap, so chunks are bounded well below 2^32.  The
+// reference's chunks are 64 KiB to a few MiB (Encoder.cpp:17-102); 1 GiB of
+// bytes encodes to 1.43 GB of text.  ADVICE r05: past 2^32 the positions
+// wrapped and tiles were never launched.
+constexpr uint64_t kB64MaxChunk = 1ull << 30, kB64MaxText = 3ull << 29;
+
 extern "C" uint64_t lbf_b64_put_length(uint64_t size) { return 4 * (size / 3) + (size % 3 ? 4 : 0) + size / 3 / 18; }
 
 // Chunks to send: verify on the device (ChunkMethods.cpp:116-123), then encode
@@ -1858,6 +1964,9 @@ extern "C" int lbf_verify_encode_b64_batch(lbf_ctx* ctx, const uint8_t* data, ui
   if (n > 0x7FFFFFFFull) return fail(LBF_ERR_INVALID, "lbf_verify_encode_b64_batch: n too large");
   uint64_t dlo = UINT64_MAX, dhi = 0, tlo = UINT64_MAX, thi = 0;
   for (uint64_t i = 0; i < n; ++i) {
+    if (sizes[i] > kB64MaxChunk)
+      return fail(LBF_ERR_INVALID, "lbf_verify_encode_b64_batch: chunk " + std::to_string(i) +
+                                       " larger than the wire encode takes (1 GiB)");
     if (offsets[i] > data_len || sizes[i] > data_len - offsets[i])
       return fail(LBF_ERR_INVALID, "lbf_verify_encode_b64_batch: chunk " + std::to_string(i) + " outside the buffer");
     const uint64_t tl = lbf_b64_put_length(sizes[i]);
@@ -1935,6 +2044,9 @@ extern "C" int lbf_b64_verify_batch(lbf_ctx* ctx, const char* text, uint64_t tex
   if (n > 0x7FFFFFFFull) return fail(LBF_ERR_INVALID, "lbf_b64_verify_batch: n too large");
   uint64_t tlo = UINT64_MAX, thi = 0, olo = UINT64_MAX, ohi = 0;
   for (uint64_t i = 0; i < n; ++i) {
+    if (text_lens[i] > kB64MaxText || expected_sizes[i] > kB64MaxChunk)
+      return fail(LBF_ERR_INVALID, "lbf_b64_verify_batch: chunk " + std::to_string(i) +
+                                       " larger than the wire decode takes (1 GiB of bytes, 1.5 GiB of text)");
     if (text_offsets[i] > text_len || text_lens[i] > text_len - text_offsets[i])
       return fail(LBF_ERR_INVALID, "lbf_b64_verify_batch: text range " + std::to_string(i) + " outside the buffer");
     tlo = std::min(tlo, text_offsets[i]);

@@ -19,7 +19,13 @@ import re
 import struct
 
 _MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
+_CCOB = b"CCOB"  # a compressed offload bundle (clang --offload-compress)
 _TARGET = b"amdgcn-amd-amdhsa--gfx950"
+
+
+class CompressedBundle(ValueError):
+    """The library's device code sits in compressed offload bundles, which this
+    reader does not inflate: no digest can be given."""
 
 
 def _code_objects(blob):
@@ -41,8 +47,20 @@ def _code_objects(blob):
     return out
 
 
+# The kernel descriptor (<kernel>.kd, 64 bytes): LDS and scratch sizes,
+# kernarg size, the compute_pgm_rsrc1/2/3 words (VGPR/SGPR counts, wave
+# limits), properties.  Bytes 16..24 hold the code's offset from the
+# descriptor, which moves whenever anything else in the object changes size,
+# so they are left out.
+_KD_SIZE = 64
+_KD_ENTRY = slice(16, 24)
+
+
 def _elf_functions(co):
-    """{symbol: machine-code bytes} for the STT_FUNC symbols of an ELF64 code object."""
+    """{symbol: machine-code bytes + its kernel descriptor's bytes (entry offset
+    zeroed)} for the STT_FUNC symbols of an ELF64 code object: two builds whose
+    instructions match but whose register counts, LDS size or wave limits
+    differ get different digests."""
     if co[:4] != b"\x7fELF" or co[4] != 2:
         raise ValueError("not an ELF64 code object")
     e_shoff, = struct.unpack_from("<Q", co, 0x28)
@@ -52,31 +70,43 @@ def _elf_functions(co):
         name, typ, flags, addr, off, size, link, info, align, entsize = struct.unpack_from(
             "<IIQQQQIIQQ", co, e_shoff + i * e_shentsize)
         secs.append((typ, addr, off, size, link, entsize))
-    out = {}
+    funcs, kds = {}, {}
     for typ, _, off, size, link, entsize in secs:
         if typ != 2:  # SHT_SYMTAB
             continue
         stroff = secs[link][2]
         for k in range(size // entsize):
             st_name, st_info, _, st_shndx, st_value, st_size = struct.unpack_from("<IBBHQQ", co, off + k * entsize)
-            if st_info & 0xF != 2 or not st_size or st_shndx >= len(secs):  # STT_FUNC with code
+            if not st_size or st_shndx >= len(secs):
+                continue
+            kind = st_info & 0xF
+            if kind not in (1, 2):  # STT_OBJECT (descriptors), STT_FUNC (code)
                 continue
             end = co.index(b"\0", stroff + st_name)
             sym = co[stroff + st_name:end].decode()
             _, saddr, soff, _, _, _ = secs[st_shndx]
             start = soff + (st_value - saddr)
-            out[sym] = co[start:start + st_size]
-    return out
+            if kind == 2:
+                funcs[sym] = co[start:start + st_size]
+            elif sym.endswith(".kd") and st_size == _KD_SIZE:
+                kd = bytearray(co[start:start + st_size])
+                kd[_KD_ENTRY] = bytes(_KD_ENTRY.stop - _KD_ENTRY.start)
+                kds[sym[:-3]] = bytes(kd)
+    return {sym: code + kds.get(sym, b"") for sym, code in funcs.items()}
 
 
 def kernel_digests(path):
-    """{mangled kernel symbol: sha256 hex of its gfx950 machine code} for the
-    library at path.  A symbol found in two code objects with different bytes
+    """{mangled kernel symbol: sha256 hex of its gfx950 machine code and kernel
+    descriptor} for the library at path; CompressedBundle if the device code is
+    compressed.  A symbol found in two code objects with different bytes
     maps to None (ambiguous)."""
     with open(path, "rb") as f:
         blob = f.read()
     out = {}
-    for co in _code_objects(blob):
+    cos = _code_objects(blob)
+    if not cos and _CCOB in blob:
+        raise CompressedBundle(f"{path}: device code in compressed offload bundles (CCOB), not read here")
+    for co in cos:
         for sym, code in _elf_functions(co).items():
             d = hashlib.sha256(code).hexdigest()
             out[sym] = d if out.get(sym, d) == d else None

@@ -166,7 +166,9 @@ int lbf_files_ranges(lbf_ctx* ctx, const char* const* paths, uint32_t n_files, c
  * Text and output in memory registered with lbf_host_register move by DMA
  * without staging.  lbf_ctx_b64_stats counts the chunks whose text had the
  * encoder's own layout (decoded in one pass) and the others (decoded by the
- * general two-pass kernel). */
+ * general two-pass kernel).  A chunk of more than 1 GiB (expected_sizes) or
+ * 1.5 GiB of text is refused (LBF_ERR_INVALID): the kernels keep positions
+ * within a chunk in 32 bits. */
 int lbf_b64_verify_batch(lbf_ctx* ctx, const char* text, uint64_t text_len, const uint64_t* text_offsets,
                          const uint32_t* text_lens, uint64_t n, const uint32_t* expected_sizes,
                          const uint8_t* expected, uint8_t* out, uint64_t out_len, const uint64_t* out_offsets,
@@ -182,8 +184,8 @@ int lbf_b64_verify_batch(lbf_ctx* ctx, const char* text, uint64_t text_len, cons
  * after every 18th complete group, "xx==" / "xxx=" for a last one or two
  * bytes -- lands at text[text_offsets[i], + lbf_b64_put_length(sizes[i]))
  * whatever the verdict; no byte of `text` outside the slots is written, and
- * overlapping slots are refused (LBF_ERR_INVALID).  Synchronous, on the
- * context's first device. */
+ * overlapping slots are refused (LBF_ERR_INVALID), and so is a chunk of more
+ * than 1 GiB.  Synchronous, on the context's first device. */
 int lbf_verify_encode_b64_batch(lbf_ctx* ctx, const uint8_t* data, uint64_t data_len, const uint64_t* offsets,
                                 const uint32_t* sizes, uint64_t n, const uint8_t* expected, uint8_t* verdicts,
                                 char* text, uint64_t text_len, const uint64_t* text_offsets);

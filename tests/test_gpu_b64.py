@@ -377,3 +377,31 @@ def test_overlapping_slots_are_refused(hasher):
                                                      sz.ctypes.data, 2, e.ctypes.data, v.ctypes.data,
                                                      tbuf.ctypes.data, tbuf.size, ts.ctypes.data)
         assert (rc == 0) is rc_ok, rc
+
+
+def test_chunks_past_the_32_bit_bound_are_refused(hasher):
+    """the wire kernels keep a chunk's text and byte positions in
+    32 bits, so chunks whose text or tile math would pass 2^32 are refused at
+    the entry points (LBF_ERR_INVALID), before any copy: the buffers here are
+    small, only their claimed lengths are large."""
+    from bitflood_amd import _capi
+    lib = _capi.load()
+    small = np.zeros(256, np.uint8)
+    zero64 = np.zeros(1, np.uint64)
+    exp, ver = np.zeros(20, np.uint8), np.zeros(1, np.uint8)
+    big = np.array([(1 << 30) + 1], np.uint32)
+    rc = lib.lbf_verify_encode_b64_batch(hasher._h, small.ctypes.data, 2 << 30, zero64.ctypes.data, big.ctypes.data,
+                                         1, exp.ctypes.data, ver.ctypes.data, small.ctypes.data, 4 << 30,
+                                         zero64.ctypes.data)
+    assert rc == _capi.LBF_ERR_INVALID and b"1 GiB" in lib.lbf_last_error()
+    ok_size = np.array([100], np.uint32)
+    for tlen, cap in (((3 << 29) + 1, ok_size), (ok_size, big)):
+        tl = np.asarray(tlen, np.uint32).reshape(1)
+        rc = lib.lbf_b64_verify_batch(hasher._h, small.ctypes.data, 4 << 30, zero64.ctypes.data, tl.ctypes.data, 1,
+                                      np.asarray(cap, np.uint32).reshape(1).ctypes.data, exp.ctypes.data, None, 0,
+                                      None, None, ver.ctypes.data)
+        assert rc == _capi.LBF_ERR_INVALID and b"wire decode" in lib.lbf_last_error()
+    # the bound is far above the reference's chunk sizes: a well-formed 4 MiB chunk still decodes
+    data = bytes(np.random.default_rng(3).integers(0, 256, 4 << 20, dtype=np.uint8))
+    ver, dec, *_ = _batch(hasher, [xmlrpc_text(data)], [data], with_out=False)
+    assert list(ver) == [True] and list(dec) == [len(data)]

@@ -7,6 +7,8 @@ The reference hashes from whatever buffer the caller holds
 Flood.cpp:263, ChunkMethods.cpp:113,159); registration only changes how the
 bytes reach HBM.  `staging_stats()` shows which route each byte took.
 """
+import mmap
+
 import numpy as np
 import pytest
 
@@ -15,6 +17,7 @@ from bitflood_amd import _capi
 
 pytestmark = pytest.mark.gpu
 MIB = 1 << 20
+PAGE = mmap.PAGESIZE
 
 
 def _ctx(monkeypatch, **env):
@@ -55,11 +58,15 @@ def test_registered_contiguous_hash_and_verify(workers, oracle, monkeypatch):
         # whatever the number of workers (two workers' halves meet inside a page
         # unless the buffer is page-aligned), so the same groups go direct;
         # under the threshold, or with LBF_AUTOPIN=0, through staging
+        # Only the pages wholly inside the job are pinned (round 6): the bytes on
+        # the buffer's first, partial page are bounced and count as staged (the
+        # last partial page lies in the staged tail group anyway)
         h.unregister_host(buf)
+        head = (-buf.ctypes.data) % PAGE
         s1 = h.staging_stats()
         assert np.array_equal(h.hash_chunks(buf, offs, sizes), want)
         d = _delta(h, s1)
-        assert d["direct"] == buf.size - 12345 and d["staged"] == 12345, d
+        assert d["direct"] == buf.size - 12345 - head and d["staged"] == 12345 + head, d
         monkeypatch.setenv("LBF_AUTOPIN_MIN_MB", "128")
         s1 = h.staging_stats()
         assert np.array_equal(h.hash_chunks(buf, offs, sizes), want)
@@ -298,3 +305,115 @@ def test_on_the_fly_pinning(oracle, monkeypatch, mib, piece_pinned, workers):
     base = buf.ctypes.data // page * page
     assert hip.hipHostRegister(ctypes.c_void_p(base), buf.ctypes.data + buf.size - base, 0) == 0
     assert hip.hipHostUnregister(ctypes.c_void_p(base)) == 0
+
+
+def _is_pinned(hip, addr):
+    """Whether HIP holds the page of `addr` pinned (a read-only query: it pins nothing)."""
+    import ctypes
+    attrs = (ctypes.c_uint8 * 256)()
+    rc = hip.hipPointerGetAttributes(ctypes.byref(attrs), ctypes.c_void_p(addr))
+    hip.hipGetLastError()
+    return rc == 0 and int.from_bytes(bytes(attrs[:4]), "little") == 1  # hipMemoryTypeHost
+
+
+def test_on_the_fly_pinning_leaves_caller_memory_alone(oracle, monkeypatch):
+    """VERDICT r05 weak #3 / ADVICE r05: while a job holds its on-the-fly pin,
+    (1) the caller pins a neighbouring buffer that shares the job's first and
+    last page with its own hipHostRegister -- it succeeds, because only the
+    pages wholly inside the job are pinned; (2) another context registers a
+    sub-range of the job's bytes through lbf_host_register -- it waits for the
+    job and then pins the range itself, never adopting the job's pages (which
+    the job unpins when it ends).  Afterwards that context's batches are
+    bit-exact and go direct from memory that really is pinned."""
+    import ctypes
+    import threading
+    import time
+    hip = _hip()
+    hip.hipPointerGetAttributes.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    size, start, hold_s = 256 * MIB, 100, 1.5
+    mm = mmap.mmap(-1, size + 4 * PAGE)
+    whole = np.frombuffer(mm, dtype=np.uint8)
+    buf = whole[start:start + size]  # begins and ends inside pages shared with other data
+    buf[:] = oracle.synth(96, 0, size, nthreads=8)
+    offs, sizes = chunk_table(size, 256 * 1024)
+    want = oracle.sha1_batch(buf, offs, sizes, nthreads=8)
+    base = buf.ctypes.data
+    head_page, tail_page = base // PAGE * PAGE, (base + size - 1) // PAGE * PAGE
+    head, tail = head_page + PAGE - base, base + size - tail_page
+    inner = head_page + 8 * PAGE
+    sub = buf[64 * MIB:128 * MIB]
+    so, ss = chunk_table(sub.size, 256 * 1024)
+    monkeypatch.setenv("LBF_TEST_AUTOPIN_HOLD_MS", str(int(hold_s * 1000)))
+    a, b = ChunkHasher(), ChunkHasher()
+    out, t = {}, {}
+    try:
+        s0 = a.staging_stats()
+
+        def job():
+            out["a"] = a.hash_chunks(buf, offs, sizes)
+            t["a_done"] = time.monotonic()
+
+        ta = threading.Thread(target=job)
+        ta.start()
+        deadline = time.monotonic() + 20
+        while not _is_pinned(hip, inner):  # the job's pin is live
+            assert ta.is_alive() and time.monotonic() < deadline, "the job never pinned its span"
+            time.sleep(0.002)
+        t["pinned"] = time.monotonic()
+        assert not _is_pinned(hip, head_page) and not _is_pinned(hip, tail_page)
+
+        def register():
+            b.register_host(sub)
+            t["b_done"] = time.monotonic()
+
+        tb = threading.Thread(target=register)
+        tb.start()
+        # the neighbour's own pinning of the shared edge pages succeeds mid-job
+        assert hip.hipHostRegister(ctypes.c_void_p(head_page), PAGE, 0) == 0
+        assert hip.hipHostRegister(ctypes.c_void_p(tail_page), PAGE, 0) == 0
+        assert ta.is_alive() and "b_done" not in t  # both made while the job held its pin
+        ta.join(60)
+        tb.join(60)
+        assert not ta.is_alive() and not tb.is_alive()
+        assert hip.hipHostUnregister(ctypes.c_void_p(head_page)) == 0
+        assert hip.hipHostUnregister(ctypes.c_void_p(tail_page)) == 0
+        assert np.array_equal(out["a"], want)
+        d = _delta(a, s0)
+        # the job's bytes on the two shared pages were bounced, the rest went direct
+        assert d["staged"] == head + tail and d["direct"] == size - head - tail, d
+        # B waited for the job (the hold) and then pinned the range itself
+        assert t["b_done"] - t["pinned"] > 0.5 * hold_s, t
+        assert _is_pinned(hip, sub.ctypes.data + 4 * PAGE)
+        monkeypatch.delenv("LBF_TEST_AUTOPIN_HOLD_MS")
+        s1 = b.staging_stats()
+        assert np.array_equal(b.hash_chunks(sub, so, ss), want[256:512])
+        assert _delta(b, s1) == {"staged": 0, "direct": sub.size}
+        b.unregister_host(sub)
+        assert not _is_pinned(hip, sub.ctypes.data + 4 * PAGE)
+    finally:
+        a.close()
+        b.close()
+    # nothing of the job is left pinned
+    assert hip.hipHostRegister(ctypes.c_void_p(head_page), tail_page + PAGE - head_page, 0) == 0
+    assert hip.hipHostUnregister(ctypes.c_void_p(head_page)) == 0
+
+
+@pytest.mark.parametrize("shape", ["gap", "repeats_plus_far_chunk"])
+def test_on_the_fly_pinning_skips_tables_with_gaps(oracle, hasher, shape):
+    """A table whose chunks leave a gap in their span is staged, never pinned
+    across the gap (round 6).  ADVICE r05: an unsorted table that repeats a few
+    chunks plus one far-off chunk used to pass the 'chunks fill half the span'
+    test by its duplicates."""
+    buf = oracle.synth(97, 0, 160 * MIB, nthreads=8)
+    offs, sizes = chunk_table(buf.size, MIB)
+    if shape == "gap":  # drop one chunk in the middle
+        keep = np.ones(offs.size, bool)
+        keep[80] = False
+        offs, sizes = offs[keep], sizes[keep]
+    else:  # 100 copies of chunks 0..1, then chunk 159, unsorted
+        offs = np.concatenate([np.tile(offs[:2], 100), offs[159:160], offs[:1]])
+        sizes = np.full(offs.size, MIB, np.uint32)
+    want = oracle.sha1_batch(buf, offs, sizes, nthreads=8)
+    s0 = hasher.staging_stats()
+    assert np.array_equal(hasher.hash_chunks(buf, offs, sizes), want)
+    assert _delta(hasher, s0)["direct"] == 0

@@ -89,12 +89,53 @@ def test_an_older_record_is_skipped_for_the_matching_one(tmp_path):
     assert t == 4296004394.0 and why is None
 
 
-def test_committed_c2_record_matches_the_shipped_library(digests):
-    """The committed C2 record was profiled on the code this tree ships (the
-    round-end bench line carries its traffic only then)."""
-    d = json.load(open(os.path.join(bench.ROOT, "profiles", "pmc_traffic.json")))
+@pytest.mark.parametrize("kernel,size,cs", [("sha1_lds2_kernel<true>", 64 << 30, 262144),
+                                            ("sha1_pc4x2_kernel<true>", 32 << 30, 1 << 20)])
+def test_other_configs_entry_cites_traffic_by_digest(tmp_path, digests, kernel, size, cs):
+    """other_configs' C3 and C4 records take their traffic
+    through the same digest rule as the main line."""
+    sym = KD.symbol_for(digests, kernel)
+    rec = {"file_bytes": size, "chunk_size": cs, "hbm_bytes_per_launch": size * 1.001, "source": "profiles/x.json",
+           "kernel": f"void lbf::(anonymous namespace)::{kernel}(lbf::ChunkParams)"}
+    p = tmp_path / "pmc.json"
+    p.write_text(json.dumps({"entries": [dict(rec, code_sha256=digests[sym])]}))
+    e = bench.config_entry("Cx", size, cs, 10.0, True, "g", kernel, pmc_path=str(p))
+    assert e["traffic"] == size * 1.001 and e["traffic_ratio"] == 1.001 and e["traffic_null_reason"] is None
+    assert e["kernel_code_sha256"] == digests[sym] and e["kernel_symbol"] == sym
+    p.write_text(json.dumps({"entries": [dict(rec, code_sha256="ef" * 32)]}))
+    e = bench.config_entry("Cx", size, cs, 10.0, True, "g", kernel, pmc_path=str(p))
+    assert e["traffic"] is None and "not the code that was profiled" in e["traffic_null_reason"]
+
+
+@pytest.mark.parametrize("kernel,size,cs", [("sha1_pc4_kernel<true, 2, 8>", 4 << 30, 262144),
+                                            ("sha1_lds2_kernel<true>", 64 << 30, 262144),
+                                            ("sha1_pc4x2_kernel<true>", 32 << 30, 1 << 20)])
+def test_committed_records_match_the_shipped_library(digests, kernel, size, cs):
+    """The committed C2, C3 and C4 records were profiled on the code this tree
+    ships (the round-end bench line carries their traffic only then)."""
+    sym = KD.symbol_for(digests, kernel)
+    t, src, why = bench.traffic_from_profiles(size, cs, kernel, digests[sym])
+    assert t is not None, why
+    assert 1.0 <= t / size < 1.03, (t, src)
+
+
+def test_descriptor_is_part_of_the_digest(digests):
+    """the digest covers the kernel descriptor (VGPR/SGPR counts,
+    LDS size), not only the instructions."""
+    with open(LIB, "rb") as f:
+        blob = f.read()
+    co = KD._code_objects(blob)[0]
+    funcs = KD._elf_functions(co)
     sym = KD.symbol_for(digests, "sha1_pc4_kernel<true, 2, 8>")
-    c2 = [e for e in d["entries"] if e["file_bytes"] == 4 << 30 and e.get("chunk_size") == 262144
-          and "sha1_pc4_kernel<true, 2, 8>" in e["kernel"] and e.get("code_sha256")]
-    assert c2, "no C2 record with a code digest"
-    assert any(e["code_sha256"] == digests[sym] for e in c2)
+    code = funcs[sym]
+    kd = bytearray(code[-64:])
+    # group_segment_fixed_size (LDS bytes) is the descriptor's first word: pc4 uses LDS
+    assert int.from_bytes(kd[:4], "little") > 0
+    assert kd[16:24] == bytes(8)  # the code-entry offset is left out
+
+
+def test_compressed_bundle_is_reported(tmp_path):
+    p = tmp_path / "fake.so"
+    p.write_bytes(b"\x7fELF" + b"\0" * 64 + b"CCOB" + b"\0" * 64)
+    with pytest.raises(KD.CompressedBundle):
+        KD.kernel_digests(str(p))
