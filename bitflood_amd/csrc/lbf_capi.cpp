@@ -907,23 +907,26 @@ constexpr uint64_t kJoinGap = 4096;
 // knob) caps the job size that goes direct; by default every size does.
 constexpr uint64_t kDirectMinRun = 1ull << 20;
 
-// Pinning a large pageable job on the fly (on by default
-// since round 5, LBF_AUTOPIN=0 turns it off).  A pageable job crosses host DRAM
-// three times on the staged route (the caller's write, the staging memcpy's
-// read and write, the DMA's read) and its rate moves with the box's memcpy; a
-// registered one crosses it once (§3).  On this ROCm, hipHostRegister of a
-// whole 4 GiB job costs about 0.1 ms (tools/autopin_probe.py), so run_job
-// registers the job's address span in one piece before any worker starts and
-// unregisters it after every worker has drained; the workers see a registered
-// source and take the direct route (measured against the staging memcpy on one
-// box, profiles/r05/autopin/: 64 MiB 14.2 against 13.0, 1 GiB 45.2 against
-// 41.8, 4 GiB 50.7 against 49.6 GiB/s).  One registration per JOB, not per
-// worker: the workers' index ranges meet inside a page unless the buffer is
-// page-aligned, and two registrations of one page are refused below (round 5
-// first pinned per worker, and with two workers one of them staged).  Pinning
-// windows ahead of the copies from a helper thread measured slower (46.8 GiB/s
-// at 4 GiB, same profile) and was dropped.  A span HIP refuses to register is
-// staged, and so is a batch whose copy HIP refuses (see worker_run).
+// Pinning a large pageable job on the fly (opt-in with
+// LBF_AUTOPIN=1: on by default in round 5, off since round 6).  A pageable job
+// crosses host DRAM three times on the staged route (the caller's write, the
+// staging memcpy's read and write, the DMA's read); a registered one once (§3).
+// Round 5 timed hipHostRegister of a 4 GiB span at ~0.1 ms and turned this on,
+// but that span had been registered before in the same process: on pages
+// registered for the first time it costs ~190 ms per 4 GiB of touched memory
+// (~21 GiB/s, ~740 ms when the pages were never touched), and only re-registering
+// pages HIP has seen is cheap (tools/register_cost.py, profiles/r06/).  So a
+// job on a fresh buffer ran 3.3x slower pinned than staged at 4 GiB (269 against
+// 81 ms) and 2.9x at 1 GiB, while a warm one gained 0-8 %.  A caller that hashes
+// one buffer repeatedly registers it once (lbf_host_register); LBF_AUTOPIN=1
+// pins each large job's pages for the job.  When on, run_job registers them in
+// one piece before any worker starts and unregisters after every worker has
+// drained; the workers see a registered source and take the direct route.  One
+// registration per JOB, not per worker: the workers' index ranges meet inside
+// a page unless the buffer is page-aligned, and two registrations of one page
+// are refused below (round 5 first pinned per worker, and with two workers one
+// of them staged).  A span HIP refuses to register is staged, and so is a
+// batch whose copy HIP refuses (see worker_run).
 //
 // The pages pinned on the fly by running jobs, process-wide, [lo, hi) each.
 // Two contexts hashing the same pageable buffer at once must not both register
@@ -1006,7 +1009,7 @@ class AutoPin {
 // filled half of).  A span larger than half of the host's physical memory is
 // staged too: pinning it would lock most of RAM for the length of the call.
 std::unique_ptr<AutoPin> pin_on_the_fly(const Job& job, uint64_t n) {
-  if (job.src.from_files() || job.src.pinned || env_long("LBF_AUTOPIN", 1) != 1) return nullptr;
+  if (job.src.from_files() || job.src.pinned || env_long("LBF_AUTOPIN", 0) != 1) return nullptr;
   const uint64_t min_bytes = env_u64("LBF_AUTOPIN_MIN_MB", 64) << 20;
   uint64_t lo = UINT64_MAX, hi = 0, sum = 0;
   bool sorted = true;

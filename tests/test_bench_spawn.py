@@ -131,6 +131,10 @@ def _check_line(out, n):
     assert "rank 0 alone" in cb["when"]
     assert out["parity"]["per_rank"] == [-1] * n  # no golden at this size
     assert out["e2e"]["parity"] is True and out["e2e"]["parity_per_rank"] == [1] * n
+    # the default route (staging), the opt-in on-the-fly route with its first pass, the caller's registration
+    for leg in ("pageable", "autopin", "registered"):
+        assert len(out["e2e"][leg]["per_rank_gibs"]) == n and out["e2e"][leg]["aggregate_gibs"] > 0, leg
+    assert len(out["e2e"]["autopin"]["first_pass_per_rank_gibs"]) == n
     assert "error" not in out["e2e_inprocess"], out["e2e_inprocess"]
     assert out["e2e_inprocess"]["parity"] is True and out["e2e_inprocess"]["parity_per_slice"] == [1] * n
     assert 0 <= out["e2e_inprocess"]["pageable_direct_fraction"] <= 1

@@ -53,15 +53,20 @@ def test_registered_contiguous_hash_and_verify(workers, oracle, monkeypatch):
         exp[flips, 19] ^= 1
         v = h.verify_chunks(buf, offs, sizes, exp)
         assert np.flatnonzero(~v).tolist() == flips
-        # unregistered: pinned on the fly for the job (the default since round 5,
-        # jobs of LBF_AUTOPIN_MIN_MB = 64 MiB and more), once for the whole job
-        # whatever the number of workers (two workers' halves meet inside a page
-        # unless the buffer is page-aligned), so the same groups go direct;
-        # under the threshold, or with LBF_AUTOPIN=0, through staging
+        # unregistered: staged by default (round 6); with LBF_AUTOPIN=1 pinned on
+        # the fly for the job (jobs of LBF_AUTOPIN_MIN_MB = 64 MiB and more), once
+        # for the whole job whatever the number of workers (two workers' halves
+        # meet inside a page unless the buffer is page-aligned), so the same
+        # groups go direct; under the threshold, or with LBF_AUTOPIN=0, staged.
         # Only the pages wholly inside the job are pinned (round 6): the bytes on
         # the buffer's first, partial page are bounced and count as staged (the
         # last partial page lies in the staged tail group anyway)
         h.unregister_host(buf)
+        s1 = h.staging_stats()
+        assert np.array_equal(h.hash_chunks(buf, offs, sizes), want)
+        d = _delta(h, s1)
+        assert d["direct"] == 0 and d["staged"] == buf.size, d
+        monkeypatch.setenv("LBF_AUTOPIN", "1")
         head = (-buf.ctypes.data) % PAGE
         s1 = h.staging_stats()
         assert np.array_equal(h.hash_chunks(buf, offs, sizes), want)
@@ -270,14 +275,15 @@ def test_buffer_the_caller_pinned_whole_goes_direct(oracle, hasher, size):
 @pytest.mark.parametrize("workers", [1, 3])
 @pytest.mark.parametrize("mib,piece_pinned", [(600, False), (600, True)])
 def test_on_the_fly_pinning(oracle, monkeypatch, mib, piece_pinned, workers):
-    """A large pageable job is pinned on the fly: its whole
-    span in one registration made before the workers start, whatever their
-    number.  It goes the direct route and leaves nothing pinned behind; a batch
+    """With LBF_AUTOPIN=1 (opt-in since round 6) a large pageable job is pinned on
+    the fly: the pages wholly inside it, in one
+    registration made before the workers start, whatever their number.  It goes the direct route and leaves nothing pinned behind; a batch
     HIP cannot copy from (part of it pinned elsewhere) is staged.  Digests equal
     the oracle's either way."""
     import ctypes
     hip = _hip()
     hasher = _ctx(monkeypatch, LBF_WORKERS_PER_DEVICE=workers)
+    monkeypatch.setenv("LBF_AUTOPIN", "1")
     buf = oracle.synth(95, 0, mib * MIB + 4321, nthreads=8)
     offs, sizes = chunk_table(buf.size, 256 * 1024)
     want = oracle.sha1_batch(buf, offs, sizes, nthreads=8)
@@ -344,6 +350,7 @@ def test_on_the_fly_pinning_leaves_caller_memory_alone(oracle, monkeypatch):
     sub = buf[64 * MIB:128 * MIB]
     so, ss = chunk_table(sub.size, 256 * 1024)
     monkeypatch.setenv("LBF_TEST_AUTOPIN_HOLD_MS", str(int(hold_s * 1000)))
+    monkeypatch.setenv("LBF_AUTOPIN", "1")
     a, b = ChunkHasher(), ChunkHasher()
     out, t = {}, {}
     try:
@@ -399,7 +406,7 @@ def test_on_the_fly_pinning_leaves_caller_memory_alone(oracle, monkeypatch):
 
 
 @pytest.mark.parametrize("shape", ["gap", "repeats_plus_far_chunk"])
-def test_on_the_fly_pinning_skips_tables_with_gaps(oracle, hasher, shape):
+def test_on_the_fly_pinning_skips_tables_with_gaps(oracle, hasher, shape, monkeypatch):
     """A table whose chunks leave a gap in their span is staged, never pinned
     across the gap (round 6).  ADVICE r05: an unsorted table that repeats a few
     chunks plus one far-off chunk used to pass the 'chunks fill half the span'
@@ -414,6 +421,12 @@ def test_on_the_fly_pinning_skips_tables_with_gaps(oracle, hasher, shape):
         offs = np.concatenate([np.tile(offs[:2], 100), offs[159:160], offs[:1]])
         sizes = np.full(offs.size, MIB, np.uint32)
     want = oracle.sha1_batch(buf, offs, sizes, nthreads=8)
+    monkeypatch.setenv("LBF_AUTOPIN", "1")
     s0 = hasher.staging_stats()
     assert np.array_equal(hasher.hash_chunks(buf, offs, sizes), want)
     assert _delta(hasher, s0)["direct"] == 0
+    # the same buffer with a gap-free table is pinned (the rule, not the buffer, decided)
+    offs, sizes = chunk_table(buf.size, MIB)
+    s0 = hasher.staging_stats()
+    assert np.array_equal(hasher.hash_chunks(buf, offs, sizes), oracle.sha1_batch(buf, offs, sizes, nthreads=8))
+    assert _delta(hasher, s0)["direct"] > buf.size // 2

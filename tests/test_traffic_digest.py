@@ -129,8 +129,8 @@ def test_descriptor_is_part_of_the_digest(digests):
     sym = KD.symbol_for(digests, "sha1_pc4_kernel<true, 2, 8>")
     code = funcs[sym]
     kd = bytearray(code[-64:])
-    # group_segment_fixed_size (LDS bytes) is the descriptor's first word: pc4 uses LDS
-    assert int.from_bytes(kd[:4], "little") > 0
+    # compute_pgm_rsrc1 (VGPR/SGPR granules) sits at byte 48 of the descriptor
+    assert int.from_bytes(kd[48:52], "little") & 63 > 0
     assert kd[16:24] == bytes(8)  # the code-entry offset is left out
 
 

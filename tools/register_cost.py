@@ -3,7 +3,8 @@
 diagnostic, GPU box, one lease.)
 
 For each size (64 MiB, 1 GiB, 4 GiB) and each of two sources, on FRESH memory
-(an anonymous mmap never registered before, written once so its pages exist):
+(never registered before, written once so its pages exist; --kind picks
+4 KiB pages, transparent huge pages, or numpy's own allocation):
 
   raw HIP (hipHostRegister / hipMemcpy, no library):
     register_ms        hipHostRegister(portable) of the whole buffer
@@ -15,13 +16,13 @@ For each size (64 MiB, 1 GiB, 4 GiB) and each of two sources, on FRESH memory
     pass1_ms..pass3_ms hash_chunks over the registered buffer (direct route)
     lbf_unregister_ms  lbf_host_unregister
     autopin1/2_ms      hash_chunks on pageable fresh memory with on-the-fly pinning
-                       (the default: register + direct + unregister inside the call)
+                       (LBF_AUTOPIN=1: register + direct + unregister inside the call)
     staged1/2_ms       the same with LBF_AUTOPIN=0 (memcpy through pinned staging)
 
 A register on memory that was never written is timed too (register_untouched_ms):
 pages that do not exist yet must be faulted in by someone.  One JSON line.
 
-    python tools/register_cost.py [--sizes 64,1024,4096]
+    python tools/register_cost.py [--sizes 64,1024,4096] [--kind 4k|thp|numpy]
 """
 import argparse
 import ctypes
@@ -56,19 +57,53 @@ def ms(t0):
     return round((time.perf_counter() - t0) * 1e3, 3)
 
 
+KIND = "4k"  # --kind: how fresh buffers are backed
+
+
+class _NumpyOwner:
+    def close(self):
+        pass
+
+
 def fresh(nbytes, seed):
-    mm = mmap.mmap(-1, nbytes)
-    a = np.frombuffer(mm, dtype=np.uint8)
+    """A buffer never registered before, written once.  KIND: '4k' an anonymous
+    mmap advised MADV_NOHUGEPAGE (what glibc malloc / new[] give a C++ caller
+    when THP is 'madvise'), 'thp' one advised MADV_HUGEPAGE, 'numpy' np.empty
+    (numpy advises huge pages itself for large arrays)."""
+    if KIND == "numpy":
+        a = np.empty(nbytes, dtype=np.uint8)
+        mm = _NumpyOwner()
+    else:
+        mm = mmap.mmap(-1, nbytes)
+        mm.madvise(mmap.MADV_HUGEPAGE if KIND == "thp" else mmap.MADV_NOHUGEPAGE)
+        a = np.frombuffer(mm, dtype=np.uint8)
     a[:] = np.random.default_rng(seed).integers(0, 256, size=nbytes, dtype=np.uint8)
     return mm, a
+
+
+def anon_huge_kib():
+    try:
+        for line in open("/proc/self/smaps_rollup"):
+            if line.startswith("AnonHugePages:"):
+                return int(line.split()[1])
+    except OSError:
+        pass
+    return None
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--sizes", default="64,1024,4096")
+    ap.add_argument("--kind", choices=["4k", "thp", "numpy"], default="4k")
     a = ap.parse_args()
+    global KIND
+    KIND = a.kind
     hip = hip_lib()
-    out = {"chunk": CS, "sizes_mib": {}}
+    try:
+        thp = open("/sys/kernel/mm/transparent_hugepage/enabled").read().strip()
+    except OSError:
+        thp = None
+    out = {"chunk": CS, "kind": KIND, "thp_enabled": thp, "sizes_mib": {}}
     with ChunkHasher(device_mask=1) as h:
         for mib in [int(x) for x in a.sizes.split(",")]:
             n = mib * MIB
@@ -76,7 +111,11 @@ def main():
             dev = ctypes.c_void_p()
             assert hip.hipMalloc(ctypes.byref(dev), n) == 0
             # raw HIP on fresh memory
+            h0 = anon_huge_kib()
             mm, buf = fresh(n, mib)
+            h1 = anon_huge_kib()
+            if h0 is not None and h1 is not None:
+                r["anon_huge_fraction"] = round((h1 - h0) * 1024 / n, 3)
             p = ctypes.c_void_p(buf.ctypes.data)
             t = time.perf_counter()
             assert hip.hipHostRegister(p, n, 1) == 0
@@ -95,6 +134,7 @@ def main():
             mm.close()
             # register on memory whose pages were never written
             mm = mmap.mmap(-1, n)
+            mm.madvise(mmap.MADV_HUGEPAGE if KIND == "thp" else mmap.MADV_NOHUGEPAGE)
             addr = ctypes.addressof(ctypes.c_char.from_buffer(mm))
             t = time.perf_counter()
             rc = hip.hipHostRegister(ctypes.c_void_p(addr), n, 1)
