@@ -913,11 +913,12 @@ constexpr uint64_t kDirectMinRun = 1ull << 20;
 // staging memcpy's read and write, the DMA's read); a registered one once (§3).
 // Round 5 timed hipHostRegister of a 4 GiB span at ~0.1 ms and turned this on,
 // but that span had been registered before in the same process: on pages
-// registered for the first time it costs ~190 ms per 4 GiB of touched memory
-// (~21 GiB/s, ~740 ms when the pages were never touched), and only re-registering
-// pages HIP has seen is cheap (tools/register_cost.py, profiles/r06/).  So a
-// job on a fresh buffer ran 3.3x slower pinned than staged at 4 GiB (269 against
-// 81 ms) and 2.9x at 1 GiB, while a warm one gained 0-8 %.  A caller that hashes
+// registered for the first time it costs 168-233 ms per 4 GiB of touched 4 KiB
+// pages (the kind new[]/malloc give; 7.5 ms on transparent huge pages, ~700 ms
+// on pages never touched), and only re-registering pages HIP has seen is cheap
+// (tools/register_cost.py, profiles/r06/register_cost/).  So a job on a fresh
+// 4 KiB-page buffer ran 3.6x slower pinned than staged at 4 GiB (294 against
+// 81 ms) and 3.4x at 1 GiB, while a warm one gained 0-8 %.  A caller that hashes
 // one buffer repeatedly registers it once (lbf_host_register); LBF_AUTOPIN=1
 // pins each large job's pages for the job.  When on, run_job registers them in
 // one piece before any worker starts and unregisters after every worker has

@@ -111,12 +111,13 @@ int lbf_verify_batch(lbf_ctx* ctx, const uint8_t* base, uint64_t base_len,
  * 12 GiB/s at 64 MiB and 50 against 34-50 GiB/s at 4 GiB.
  * Meant for buffers reused across calls (a peer's receive arenas, a resident
  * file image): the first registration of pages costs about as much as one
- * staged pass over them (4 GiB of touched memory: 168-187 ms, ~21-24 GiB/s;
- * pages never touched ~5 GiB/s, the registration faults them in), and that
- * cost lands in this call, not in the first direct pass; registering pages
- * HIP registered before in the process costs ~0.1 ms; unregistering ~0.03 ms
- * (tools/register_cost.py, profiles/r06/register_cost.json).  A call that
- * overlaps pages a running job pinned on the fly (LBF_AUTOPIN=1) waits for
+ * staged pass over them -- 4 GiB of touched 4 KiB pages 168-233 ms (what new[]
+ * and malloc give), 7.5 ms on transparent huge pages, ~700 ms on pages never
+ * touched (the registration faults them in) -- and that cost lands in this
+ * call, not in the first direct copy; registering pages HIP registered before
+ * in the process is cheap, unregistering ~0.03 ms (tools/register_cost.py,
+ * profiles/r06/register_cost/).  A call that overlaps pages a running job
+ * pinned on the fly (LBF_AUTOPIN=1) waits for
  * that job to end, then pins the range itself.  Memory
  * that is already pinned is accepted and left pinned.  Pinning is per page:
  * ranges held by one context may not share a page (give each registered

@@ -84,10 +84,20 @@ int main(int argc, char** argv) {
       const uint64_t buf_len = uni(1, 12) << 20;
       std::vector<uint8_t> buf(buf_len);
       oracle_synth_fill_mt(buf.data(), buf_len, rng(), 0, 4);
-      const uint64_t n = uni(0, 1) ? uni(0, 40) : uni(0, 1500);
+      // a quarter of the tables cover a span of the buffer without a gap (from a
+      // random start byte, any chunk size): the shape on-the-fly pinning takes,
+      // its inward page rounding and the bounce of the partial edge pages
+      const bool tiled = uni(0, 3) == 0;
+      const uint64_t t_lo = tiled ? uni(0, buf_len / 4) : 0, t_cs = tiled ? uni(1, 600000) : 1;
+      const uint64_t n = tiled ? (buf_len - t_lo + t_cs - 1) / t_cs : uni(0, 1) ? uni(0, 40) : uni(0, 1500);
       std::vector<uint64_t> off(n);
       std::vector<uint32_t> size(n);
       for (uint64_t i = 0; i < n; ++i) {
+        if (tiled) {
+          off[i] = t_lo + i * t_cs;
+          size[i] = (uint32_t)std::min<uint64_t>(t_cs, buf_len - off[i]);
+          continue;
+        }
         const int kind = (int)uni(0, 9);
         uint64_t s = kind == 0 ? uni(0, 130) : kind == 1 ? uni(1, 3) << 20 : uni(0, kind < 5 ? 70000 : 300000);
         s = std::min<uint64_t>(s, buf_len);
@@ -289,6 +299,54 @@ int main(int argc, char** argv) {
       faults += done_faults.load();
       cases += 3;
       concurrent += 3;
+    }
+    if (uni(0, 2) == 0) {
+      // two contexts: a job pinned on the fly (LBF_AUTOPIN=1, read per job)
+      // while another context registers a range inside its pages, and a third
+      // thread pins the page the job shares with its neighbour (round 6: the
+      // job's pages are never adopted, the edge page is never the job's)
+      setenv("LBF_AUTOPIN", "1", 1);
+      setenv("LBF_TEST_FAULT_GROUP", "-1", 1);  // read at creation: the second context injects nothing
+      lbf_ctx* other = nullptr;
+      CHECK(lbf_ctx_create(1, &other) == LBF_OK, "second context: %s", lbf_last_error());
+      const uint64_t page = (uint64_t)sysconf(_SC_PAGESIZE), len = uni(8, 24) << 20;
+      std::vector<uint8_t> b(len + 2 * page);
+      const uint64_t skew = uni(1, page - 1);  // the job starts and ends inside shared pages
+      uint8_t* job = b.data() + skew;
+      const uint64_t jlen = len;
+      oracle_synth_fill_mt(job, jlen, rng(), 0, 2);
+      const uint64_t cs = uni(1, 3) << 18, n = (jlen + cs - 1) / cs;
+      std::vector<uint64_t> o(n);
+      std::vector<uint32_t> z(n);
+      for (uint64_t i = 0; i < n; ++i) o[i] = i * cs, z[i] = (uint32_t)std::min<uint64_t>(cs, jlen - i * cs);
+      std::vector<uint8_t> w(20 * n), g(20 * n, 0xEE);
+      for (uint64_t i = 0; i < n; ++i) oracle_sha1(job + o[i], z[i], &w[20 * i]);
+      const uint64_t sub_lo = ((uint64_t)(job - b.data()) + jlen / 4 + page - 1) / page * page;
+      uint8_t* sub = b.data() + sub_lo;
+      const uint64_t sub_len = jlen / 4;
+      std::thread a([&] {
+        const int rc = lbf_sha1_batch(ctx, job, jlen, o.data(), z.data(), n, g.data(), LBF_HOST_PTR);
+        CHECK(rc == LBF_OK || strstr(lbf_last_error(), "injected fault"), "pinned-on-the-fly job rc %d: %s", rc,
+              lbf_last_error());
+        CHECK(rc != LBF_OK || memcmp(g.data(), w.data(), 20 * n) == 0, "pinned-on-the-fly job digests");
+      });
+      std::thread r([&] {
+        CHECK(lbf_host_register(other, sub, sub_len) == LBF_OK, "register beside a job: %s", lbf_last_error());
+        std::vector<uint64_t> so{0};
+        std::vector<uint32_t> ss{(uint32_t)sub_len};
+        std::vector<uint8_t> sd(20), sw(20);
+        oracle_sha1(sub, sub_len, sw.data());
+        CHECK(lbf_sha1_batch(other, sub, sub_len, so.data(), ss.data(), 1, sd.data(), LBF_HOST_PTR) == LBF_OK,
+              "hash of the registered sub-range: %s", lbf_last_error());
+        CHECK(memcmp(sd.data(), sw.data(), 20) == 0, "registered sub-range digest");
+        CHECK(lbf_host_unregister(other, sub) == LBF_OK, "unregister: %s", lbf_last_error());
+      });
+      a.join();
+      r.join();
+      lbf_ctx_destroy(other);
+      cases += 2;
+      concurrent += 2;
+      chunks_checked += (long)n + 1;
     }
     lbf_ctx_destroy(ctx);
   }
