@@ -425,8 +425,12 @@ def test_on_the_fly_pinning_skips_tables_with_gaps(oracle, hasher, shape, monkey
     s0 = hasher.staging_stats()
     assert np.array_equal(hasher.hash_chunks(buf, offs, sizes), want)
     assert _delta(hasher, s0)["direct"] == 0
-    # the same buffer with a gap-free table is pinned (the rule, not the buffer, decided)
+    # the same buffer with a gap-free table is pinned (the rule, not the buffer, decided),
+    # in file order and shuffled with repeats (the union is measured on a sorted copy)
     offs, sizes = chunk_table(buf.size, MIB)
-    s0 = hasher.staging_stats()
-    assert np.array_equal(hasher.hash_chunks(buf, offs, sizes), oracle.sha1_batch(buf, offs, sizes, nthreads=8))
-    assert _delta(hasher, s0)["direct"] > buf.size // 2
+    perm = np.random.default_rng(9).permutation(offs.size)
+    perm = np.concatenate([perm, perm[:7]])
+    for o, z in ((offs, sizes), (offs[perm], sizes[perm])):
+        s0 = hasher.staging_stats()
+        assert np.array_equal(hasher.hash_chunks(buf, o, z), oracle.sha1_batch(buf, o, z, nthreads=8))
+        assert _delta(hasher, s0)["direct"] > buf.size // 2

@@ -656,6 +656,12 @@ __global__ void __launch_bounds__(512) sha1_pc4x2w8_kernel(ChunkParams p) {
   } else {
     // ---------------- consumer of group g ----------------
     if (kPrioC != 0) __builtin_amdgcn_s_setprio(kPrioC);
+#ifdef LBF_PC_STAMPS
+    unsigned long long acc[4] = {0, 0, 0, 0};  // a stamped build compiles this variant too (not reported)
+#define W8_ACC , acc
+#else
+#define W8_ACC
+#endif
     Digest s;
     s.init();
     Pc4Sched<2> A, B;
@@ -664,7 +670,7 @@ __global__ void __launch_bounds__(512) sha1_pc4x2w8_kernel(ChunkParams p) {
       __syncthreads();  // barrier E
       A.load_all(Pc4Sched<2>::col(ring, 0, lane));
       __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): slot 0 is free from barrier 0 on
-      pc4_barrier(s);  // barrier 0
+      pc4_barrier(s W8_ACC);  // barrier 0
     }
     uint32_t k = 0;
     const uint32_t fast_end = __builtin_amdgcn_readfirstlane(nsteps ? min(min_steps, nsteps - 1) : 0u);
@@ -672,20 +678,21 @@ __global__ void __launch_bounds__(512) sha1_pc4x2w8_kernel(ChunkParams p) {
 #pragma unroll
       for (int j = 0; j < 6; j += 2) {
         pc4_step(s, A, B, Pc4Sched<2>::col(ring, (j + 1) % kPc4x2Ring, lane), true, true);
-        pc4_barrier(s);
+        pc4_barrier(s W8_ACC);
         pc4_step(s, B, A, Pc4Sched<2>::col(ring, (j + 2) % kPc4x2Ring, lane), true, true);
-        pc4_barrier(s);
+        pc4_barrier(s W8_ACC);
       }
     }
     for (; k < nsteps; k += 2) {
       pc4_step(s, A, B, Pc4Sched<2>::col(ring, (k + 1) % kPc4x2Ring, lane), k < c.total, k < min_steps);
       if (k + 1 >= nsteps) break;
-      pc4_barrier(s);
+      pc4_barrier(s W8_ACC);
       pc4_step(s, B, A, Pc4Sched<2>::col(ring, (k + 2) % kPc4x2Ring, lane), k + 1 < c.total, k + 1 < min_steps);
       if (k + 2 >= nsteps) break;
-      pc4_barrier(s);
+      pc4_barrier(s W8_ACC);
     }
     if (i < p.n) write_result(p, i, s);
+#undef W8_ACC
   }
 }
 

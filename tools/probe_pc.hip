@@ -2,7 +2,7 @@
 // (not product code).  Compiles the product sources with LBF_PC_STAMPS and
 // prints, per role, the mean cycles per block step spent waiting vs working.
 // Build: hipcc --offload-arch=gfx950 -O3 -DLBF_PC_STAMPS -I../include -I../bitflood_amd/csrc \
-//          probe_pc.hip -o build/probe_pc
+//          probe_pc.hip -o build/probe_pc -L/opt/rocm/lib -lhsa-runtime64
 #include "../bitflood_amd/csrc/lbf_capi.cpp"
 #include "../bitflood_amd/csrc/sha1_kernels.hip"
 #include "experimental/sha1_superseded.hip"  // variants 4, 6, 13
@@ -46,6 +46,20 @@ static void run(int variant, uint8_t* buf, uint64_t len, uint32_t cs, uint8_t* d
   for (int r = 1; r < roles; ++r)
     printf(" producer%d[vmwait %.0f work %.0f barrier %.0f]", r - 1, a[r][0], a[r][1], a[r][2]);
   printf("\n");
+  if (x2) {
+    // pc4x2: the two consumers (waves 2 and 3) separately, and how often each
+    // is the one the barrier waits for (its wait below the other's)
+    double cw[2] = {0, 0};
+    long later[2] = {0, 0};
+    for (int w = 0; w < wgs; ++w) {
+      const double c0 = (double)h[(w * nw + 2) * 4 + 0], c1 = (double)h[(w * nw + 3) * 4 + 0];
+      cw[0] += c0;
+      cw[1] += c1;
+      later[c0 < c1 ? 0 : 1]++;
+    }
+    printf("  pc4x2 consumers: wave 2 waits %.0f, wave 3 waits %.0f cycles/step; arrives last in %ld / %ld of %d workgroups\n",
+           cw[0] / (wgs * steps), cw[1] / (wgs * steps), later[0], later[1], wgs);
+  }
 }
 
 int main(int argc, char** argv) {
