@@ -697,6 +697,93 @@ __global__ void __launch_bounds__(512) sha1_pc4x2w8_kernel(ChunkParams p) {
 }
 
 // ---------------------------------------------------------------------------
+// Variant 37 (round 6 A/B): pc4 with ONE workgroup barrier per TWO steps.
+// The stamped build puts pc4's consumer at ~55 cycles of barrier wait per step
+// (it arrives last; the producers wait ~480): that is the barrier's own
+// latency.  With a barrier every second step the same 4-slot ring suffices:
+// after barrier B_j the consumer runs steps 2j and 2j+1, loading 2j+1 and 2j+2
+// (complete at B_j), while producer 1 builds step 2j+3 and producer 0 step
+// 2j+4 whole, into the slots of steps 2j-1 and 2j, whose loads were drained at
+// B_j.  Before B_0 producer 0 builds steps 0 and 2, producer 1 step 1.  Both
+// sides pass B_0 and then one barrier per pair (k, k+1) with k + 2 < nsteps:
+// floor((nsteps - 1) / 2) of them.
+// ---------------------------------------------------------------------------
+template <bool kUniform, int kUnroll = 8>
+__global__ void __launch_bounds__(192) sha1_pc4b2_kernel(ChunkParams p) {
+  extern __shared__ __attribute__((aligned(16))) uint4 ring[];  // W[4][20][64] | raw[2][2][4][64]
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t i = blockIdx.x * kPcLanes + lane;
+  const ChainInfo c = chain_info<kUniform>(p, i);
+  const uint32_t nsteps = __builtin_amdgcn_readfirstlane(wave_max(c.total));
+  const uint32_t npairs = nsteps >= 1 ? (nsteps - 1) / 2 : 0u;  // barriers after B_0
+#ifdef LBF_PC_STAMPS
+  unsigned long long acc[4] = {0, 0, 0, 0};
+#define B2_ACC , acc
+#else
+#define B2_ACC
+#endif
+  if (wave != 0) {
+    const uint32_t X = wave - 1;  // producer X builds steps X, X + 2, ... in order
+    uint4* raw = ring + kPc4Ring * kPcSlotU4 + X * (kP2Raw * kPcRawU4);
+    const uint32_t raw_lds = (uint32_t)reinterpret_cast<uintptr_t>(raw);
+    p2_dma(c, X, raw_lds, 0);
+    p2_dma(c, X + 2, raw_lds, 1);
+    uint32_t w[16];
+    auto whole = [&](uint32_t step) {
+      const uint32_t j = (step - X) >> 1;
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // block j landed; only j+1's DMAs pending
+      p2_block(w, raw + (j & 1u) * kPcRawU4 + lane, c, step);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // raw slot read before it is refilled
+      p2_dma(c, step + 4, raw_lds, j & 1u);
+      pc4_store_half<2, 0>(w, ring, step, lane);
+      pc4_store_half<2, 1>(w, ring, step, lane);
+    };
+    if (nsteps > 0) {
+      if (X < nsteps) whole(X);
+      if (X == 0 && 2 < nsteps) whole(2);
+      PC4_SYNC();  // B_0: steps 0..2 complete
+    }
+    for (uint32_t j = 0; j < npairs; ++j) {
+      const uint32_t step = 2 * j + 3 + (X == 0 ? 1u : 0u);
+      if (step < nsteps) whole(step);
+      PC4_SYNC();  // B_{j+1}: steps <= 2j + 4 complete
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA outlives the workgroup
+  } else {
+    Digest s;
+    s.init();
+    Pc4Sched<2> A, B;
+    const uint32_t min_steps = __builtin_amdgcn_readfirstlane(wave_min(i < p.n ? c.total : 0xFFFFFFFFu));
+    if (nsteps > 0) {
+      PC4_SYNC();  // B_0
+      A.load_all(Pc4Sched<2>::col(ring, 0, lane));
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+    }
+    uint32_t k = 0;
+    const uint32_t fast_end = __builtin_amdgcn_readfirstlane(nsteps ? min(min_steps, nsteps - 1) : 0u);
+    static_assert(kUnroll % 4 == 0, "the fast loop keeps k % 4 == 0");
+    for (; k + kUnroll <= fast_end; k += kUnroll) {
+#pragma unroll
+      for (int j = 0; j < kUnroll; j += 2) {
+        pc4_step(s, A, B, Pc4Sched<2>::col(ring, (j + 1) % 4, lane), true, true);
+        pc4_step(s, B, A, Pc4Sched<2>::col(ring, (j + 2) % 4, lane), true, true);
+        pc4_barrier(s B2_ACC);  // after the pair
+      }
+    }
+    for (; k < nsteps; k += 2) {
+      pc4_step(s, A, B, Pc4Sched<2>::col(ring, (k + 1) % kPc4Ring, lane), k < c.total, k < min_steps);
+      if (k + 1 >= nsteps) break;
+      pc4_step(s, B, A, Pc4Sched<2>::col(ring, (k + 2) % kPc4Ring, lane), k + 1 < c.total, k + 1 < min_steps);
+      if (k + 2 >= nsteps) break;
+      pc4_barrier(s B2_ACC);
+    }
+    if (i < p.n) write_result(p, i, s);
+  }
+#undef B2_ACC
+}
+
+// ---------------------------------------------------------------------------
 // The launch table
 // ---------------------------------------------------------------------------
 using Kern = void (*)(ChunkParams);
@@ -750,6 +837,7 @@ const Entry kTable[] = {
     {34, &sha1_pc4x2w8_kernel<false, 3, 1>, &sha1_pc4x2w8_kernel<true, 3, 1>, 128, 512, kPc4x2LdsBytes},
     {35, &sha1_pc4x2w8_kernel<false, 0, 0>, &sha1_pc4x2w8_kernel<true, 0, 0>, 128, 512, kPc4x2LdsBytes},
     {36, &sha1_pc4x2w8_kernel<false, 0, 1>, &sha1_pc4x2w8_kernel<true, 0, 1>, 128, 512, kPc4x2LdsBytes},
+    {37, &sha1_pc4b2_kernel<false>, &sha1_pc4b2_kernel<true>, 64, 192, kPc4LdsBytes},
 };
 
 const Entry* find_entry(int variant) {

@@ -30,6 +30,8 @@ from tests.oracle_lib import Oracle  # noqa: E402
 # Shipped variants; with LBF_LIB pointing at the A/B library of
 # tools/experimental/ (make -C tools/experimental) LBF_FUZZ_ALL=1 adds the rest.
 VARIANTS = list(range(1, 13)) if os.environ.get("LBF_FUZZ_ALL") else [1, 7, 10, 11, 12]
+if os.environ.get("LBF_FUZZ_VARIANTS"):  # e.g. "7,37" for an A/B variant of the experimental library
+    VARIANTS = [int(x) for x in os.environ["LBF_FUZZ_VARIANTS"].split(",")]
 THREADS = min(16, os.cpu_count() or 1)
 
 
