@@ -838,6 +838,14 @@ const Entry kTable[] = {
     {35, &sha1_pc4x2w8_kernel<false, 0, 0>, &sha1_pc4x2w8_kernel<true, 0, 0>, 128, 512, kPc4x2LdsBytes},
     {36, &sha1_pc4x2w8_kernel<false, 0, 1>, &sha1_pc4x2w8_kernel<true, 0, 1>, 128, 512, kPc4x2LdsBytes},
     {37, &sha1_pc4b2_kernel<false>, &sha1_pc4b2_kernel<true>, 64, 192, kPc4LdsBytes},
+    // round 6: one pc4x2 group per workgroup at its own 76 KiB, so TWO workgroups
+    // share a CU, each with its own barrier (no coupling of the two consumers),
+    // at the price of SIMD placement the launch does not control; 38 with the
+    // consumer at priority 3, 39 without
+    {38, &sha1_pc4x2_diag_kernel<false, 1, true, 3, false, 6, true>,
+     &sha1_pc4x2_diag_kernel<true, 1, true, 3, false, 6, true>, 64, 192, kPc4x2GroupU4 * 16},
+    {39, &sha1_pc4x2_diag_kernel<false, 1, true, 3, false, 6>, &sha1_pc4x2_diag_kernel<true, 1, true, 3, false, 6>,
+     64, 192, kPc4x2GroupU4 * 16},
 };
 
 const Entry* find_entry(int variant) {
