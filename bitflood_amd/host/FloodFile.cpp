@@ -117,15 +117,25 @@ struct Parser {
       else if (ent == "quot") out += '"';
       else if (ent == "apos") out += '\'';
       else if (!ent.empty() && ent[0] == '#') {
-        unsigned long cp = ent.size() > 1 && (ent[1] == 'x' || ent[1] == 'X') ? strtoul(ent.c_str() + 2, nullptr, 16)
-                                                                            : strtoul(ent.c_str() + 1, nullptr, 10);
-        if (cp < 0x80) {
+        const bool hex = ent.size() > 1 && (ent[1] == 'x' || ent[1] == 'X');
+        const char* digits = ent.c_str() + (hex ? 2 : 1);
+        char* end = nullptr;
+        const unsigned long cp = strtoul(digits, &end, hex ? 16 : 10);
+        // a character reference names one XML Char (XML 1.0 §2.2): not empty,
+        // no trailing junk, no surrogate, nothing past U+10FFFF
+        if (end == digits || *end != '\0' || cp == 0 || cp > 0x10FFFF || (cp >= 0xD800 && cp <= 0xDFFF)) return false;
+        if (cp < 0x80) {  // UTF-8, one to four bytes
           out += (char)cp;
-        } else if (cp < 0x800) {  // UTF-8
+        } else if (cp < 0x800) {
           out += (char)(0xC0 | (cp >> 6));
           out += (char)(0x80 | (cp & 0x3F));
-        } else {
+        } else if (cp < 0x10000) {
           out += (char)(0xE0 | (cp >> 12));
+          out += (char)(0x80 | ((cp >> 6) & 0x3F));
+          out += (char)(0x80 | (cp & 0x3F));
+        } else {  // round 6: characters past the BMP took three bytes and lost their top bits
+          out += (char)(0xF0 | (cp >> 18));
+          out += (char)(0x80 | ((cp >> 12) & 0x3F));
           out += (char)(0x80 | ((cp >> 6) & 0x3F));
           out += (char)(0x80 | (cp & 0x3F));
         }
