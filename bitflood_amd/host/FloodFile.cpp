@@ -101,9 +101,18 @@ struct Parser {
     }
   }
 
+  // An attribute value as an XML 1.0 parser reports it (§3.3.3, what Xerces
+  // hands FloodFile.cpp:74): line ends normalised (CR LF or a lone CR is one
+  // LF, §2.11), every literal TAB, LF or CR then a space, entity and character
+  // references replaced (a reference to TAB, LF or CR keeps that character).
   static bool decode(const std::string& raw, std::string& out) {
     out.clear();
     for (size_t i = 0; i < raw.size(); ++i) {
+      if (raw[i] == '\r' || raw[i] == '\n' || raw[i] == '\t') {
+        if (raw[i] == '\r' && i + 1 < raw.size() && raw[i + 1] == '\n') ++i;
+        out += ' ';
+        continue;
+      }
       if (raw[i] != '&') {
         out += raw[i];
         continue;
